@@ -1,0 +1,299 @@
+"""Benchmark: SGNS pair-updates/sec at d=128 on a 1M-node power-law graph (BASELINE.json metric,
+configs[2] = SURVEY.md §8d C3), 1..8 MI355X, walk shard + periodic RCCL delta all-reduce.
+
+One "step" = one O2 launch (come_sgns_o2, Hogwild, one wavefront per walk) over a batch of
+`--walks-per-step` random walks already resident in HBM, plus -- for N > 1, every `--sync-every`
+steps -- the delta all-reduce of both embedding tables over RCCL.  Every rank trains its own walk
+shard (weak scaling).  Printed by rank 0: ONE JSON line (contract in the task statement), with
+`roofline` (dominant kernel: achieved algorithmic HBM bytes / launch time vs the 8 TB/s peak) and,
+at N = 1, `cpu_baseline` (the reference's own Cython train_o2, built by oracle/build_ref.py, timed
+on this host's cores with Python worker threads exactly as Context2Vec drives it).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def o2_pairs_of_lengths(lengths, w):
+    """Pairs train_o2 makes on a walk of l valid leading entries (pyx:494-506)."""
+    import torch
+    l = lengths.long()
+    full = 2 * w * l - w * (w + 1)
+    small = l * (l - 1)
+    return torch.where(l >= w + 1, full, small).sum()
+
+
+def cpu_reference_baseline(graph_walks_np, node_np, ctx_np, table_np, window, neg, lr,
+                           seconds, threads):
+    """Time the reference's Cython train_o2 (oracle/_ref) on host cores, driven like
+    Context2Vec.train (context_embeddings.py:72-98): worker threads, one call per walk, GIL
+    released inside.  Returns (pairs/s, pairs, walks) or None when the module is absent."""
+    import importlib.util
+    so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "training_sdg_inner*.so"))
+    if not so:
+        return None
+    spec = importlib.util.spec_from_file_location("training_sdg_inner", so[0])
+    ref = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref)
+
+    class Vocab(object):
+        __slots__ = ("index",)
+
+        def __init__(self, i):
+            self.index = i
+
+    cache = {}
+
+    def path_of(row):
+        out = []
+        for r in row:
+            if r < 0:
+                break
+            v = cache.get(r)
+            if v is None:
+                v = cache[r] = Vocab(int(r))
+            out.append(v)
+        return out
+
+    walks = [path_of(r) for r in graph_walks_np]
+    counter = {"next": 0, "pairs": 0, "walks": 0}
+    lock = threading.Lock()
+    deadline = [0.0]
+    d = node_np.shape[1]
+
+    def pairs_of(l):
+        return 2 * window * l - window * (window + 1) if l >= window + 1 else l * (l - 1)
+
+    def worker():
+        work = np.zeros(d, np.float32)
+        while True:
+            with lock:
+                i = counter["next"]
+                if i >= len(walks) or time.time() > deadline[0]:
+                    return
+                counter["next"] = i + 1
+            ref.train_o2(node_np, ctx_np, walks[i], lr, neg, window, table_np, py_alpha=1.0,
+                         py_size=d, py_work=work)
+            with lock:
+                counter["pairs"] += pairs_of(len(walks[i]))
+                counter["walks"] += 1
+
+    ts = [threading.Thread(target=worker, daemon=True) for _ in range(threads)]
+    t0 = time.time()
+    deadline[0] = t0 + seconds
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.time() - t0
+    return counter["pairs"] / el, counter["pairs"], counter["walks"], el
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--mean-degree", type=float, default=20.0)  # -> ~10M undirected edges
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--window", type=int, default=5)
+    ap.add_argument("--walk-length", type=int, default=80)
+    ap.add_argument("--walks-per-step", type=int, default=1 << 17)
+    ap.add_argument("--table-size", type=int, default=100_000_000)
+    ap.add_argument("--lr", type=float, default=0.025)
+    ap.add_argument("--sync-every", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import come_amd.training_sdg_inner as tsi
+    from come_amd.distributed import DeltaAllReduce
+    from come_amd.graph import chung_lu, random_walks
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---- workload: C3 (same graph on every rank; walks sharded by rank) ----
+    t0 = time.time()
+    g = chung_lu(args.nodes, args.mean_degree, gamma=2.5, seed=1)
+    V, d, n, w, L = g.V, args.dim, args.negative, args.window, args.walk_length
+    from come_amd.model import Model
+    np.random.seed(1234)
+    model = Model(g.degree_by_id(), size=d, table_size=args.table_size, k=1, device=dev)
+    if rank == 0:
+        log("graph V=%d E=%d (%.1fs); tables %.0f MB each; negative table %.0f MB" % (
+            V, g.num_edges, time.time() - t0, V * d * 4 / 1e6, args.table_size * 4 / 1e6))
+    B = args.walks_per_step
+    total_steps = args.warmup + args.steps
+    passes = (total_steps * B + V - 1) // V
+    walks_all = random_walks(g, passes, L, seed=100 + rank, device=dev)[:total_steps * B]
+    walks_all = walks_all.contiguous()
+    np.random.seed(5678 + rank)
+    seeds_all = torch.from_numpy(tsi.draw_seeds(total_steps * B).view(np.int64)).to(dev)
+    lengths = (walks_all >= 0).sum(dim=1)
+    pairs_per_step = [int(o2_pairs_of_lengths(lengths[s * B:(s + 1) * B], w))
+                      for s in range(total_steps)]
+    sync = DeltaAllReduce([model.node_embedding, model.context_embedding]) if world > 1 else None
+
+    def step(s):
+        tsi.sgns_o2(model.node_embedding, model.context_embedding, walks_all[s * B:(s + 1) * B],
+                    seeds_all[s * B:(s + 1) * B], w, n, model.table, args.lr, 1.0,
+                    tsi.MODE_HOGWILD)
+
+    stream = torch.cuda.current_stream(dev)
+    for s in range(args.warmup):
+        step(s)
+        if sync is not None and (s + 1) % args.sync_every == 0:
+            sync.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        s = args.warmup + k
+        ev[k][0].record(stream)
+        step(s)
+        ev[k][1].record(stream)
+        if sync is not None and (k + 1) % args.sync_every == 0:
+            sync.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        pt = torch.tensor([sum(pairs_per_step[args.warmup:])], dtype=torch.float64, device=dev)
+        dist.all_reduce(pt, op=dist.ReduceOp.SUM)
+        total_pairs = float(pt.item())
+    else:
+        total_pairs = float(sum(pairs_per_step[args.warmup:]))
+
+    assert torch.isfinite(model.node_embedding).all() and torch.isfinite(
+        model.context_embedding).all(), "non-finite embedding after training"
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    bytes_per_pair = 2 * (2 + n) * d * 4  # in row r+w, (1+n) out rows r+w
+    pairs_rank_step = float(np.mean(pairs_per_step[args.warmup:]))
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    achieved = bytes_per_pair * pairs_rank_step / avg_kernel_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if (tj.get("walks_per_launch") == B and tj.get("dim") == d
+                    and tj.get("negative") == n):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sample = min(60000, B)
+        wn = walks_all[:sample].cpu().numpy()
+        node_h = np.ascontiguousarray(model.node_embedding.cpu().numpy())
+        ctx_h = np.ascontiguousarray(model.context_embedding.cpu().numpy())
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        r = cpu_reference_baseline(wn, node_h, ctx_h, model.table_host, w, n, args.lr,
+                                   args.cpu_seconds, threads)
+        if r is not None:
+            rate, cp, cw, cel = r
+            cpu = {"value": rate, "unit": "pair-updates/s", "cores": threads,
+                   "kind": "reference",
+                   "sample": "reference Cython train_o2 (oracle/_ref, built from "
+                             "utils/training_sdg_inner.pyx) driven by %d Python threads like "
+                             "Context2Vec.train; %d walks / %d pair-updates of this workload "
+                             "(same graph, tables, negative table) in %.1fs" % (
+                                 threads, cw, cp, cel)}
+        else:
+            log("oracle/_ref absent: no reference CPU baseline")
+
+    value = total_pairs / elapsed
+    out = {
+        "metric": "SGNS pair-updates/sec at d=128, 1M-node graph",
+        "value": value,
+        "unit": "pair-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: Chung-Lu power-law graph (gamma 2.5) + uniform random walks, "
+                "tables initialised as the reference (node U(-1,1), ctx 0)",
+        "config": {
+            "workload": "configs[2]/C3: O2 SGNS over random walks, power-law %d nodes / %d "
+                        "edges, d=%d, negative=%d, window=%d, walk_length=%d, table_size=%d" % (
+                            V, g.num_edges, d, n, w, L, args.table_size),
+            "walks_per_step_per_gpu": B,
+            "pairs_per_step_per_gpu": pairs_rank_step,
+            "sync_every_steps": args.sync_every if world > 1 else None,
+            "parallelism": "walk-shard dp%d + delta all-reduce (RCCL)" % world if world > 1
+            else "single GPU, Hogwild over walks",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "come::k_sgns_o2<2,true,5>",
+            "bytes_per_pair": bytes_per_pair,
+            "avg_kernel_ms": avg_kernel_s * 1e3,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

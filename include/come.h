@@ -1,0 +1,115 @@
+/*
+ * come.h -- C-ABI of the MI355X-native ComE hot path (libcome.so, gfx950).
+ *
+ * Drop-in boundary for the reference's Cython kernel module
+ * (`from utils.training_sdg_inner import train_o1, train_o2, FAST_VERSION`,
+ *  /root/reference/ADSCModel/node_embeddings.py:13, context_embeddings.py:14) and for the numpy /
+ * sklearn hot loops of /root/reference/ADSCModel/community_embeddings.py.
+ *
+ * Conventions
+ *  - Every pointer named "device" is a non-owning device pointer (the caller owns the buffer, e.g.
+ *    a torch tensor); tables are C-contiguous row-major fp32 [rows x d], exactly the layout the
+ *    reference's numpy arrays have (pyx:410-411,457-459).
+ *  - `stream` is a hipStream_t passed as void* (NULL = the default stream).  Calls are
+ *    asynchronous on that stream, capture-safe (no allocation / synchronisation inside) once
+ *    come_init() has run for the device, and reentrant per stream.
+ *  - Return value: 0 = ok, < 0 = error (COME_E_*); come_last_error() returns a message
+ *    (thread-local).  The reference checks nothing (bounds checks off, cython_utils.py:7); this
+ *    library validates shapes/arguments on the host and never reads or writes out of bounds on
+ *    the device: walk entries outside [0, V) are treated as None (pyx:435-436), table draws
+ *    outside [0, V) are skipped.
+ *  - Row index = the reference's Vocab.index (rank of the node id, model.py:60-64).
+ */
+#ifndef COME_H_
+#define COME_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COME_ABI_VERSION 1
+
+enum {
+    COME_OK = 0,
+    COME_E_INVALID = -1, /* bad argument (message in come_last_error) */
+    COME_E_HIP = -2,     /* HIP runtime error */
+    COME_E_UNSUPPORTED = -3
+};
+
+enum {
+    COME_MODE_HOGWILD = 0,    /* one wavefront per walk/edge, all walks/edges in flight (the
+                                 reference's per-walk Hogwild threads, pyx:493) */
+    COME_MODE_SEQUENTIAL = 1  /* one wavefront, walks/edges in order == workers=1: the parity
+                                 anchor, bit-exact with oracle/ in its WAVE64 dot order */
+};
+
+int come_abi_version(void);
+const char *come_last_error(void);
+
+/* Uploads the sigmoid table (pyx:531-533) to `device`'s constant memory.  Called implicitly by the
+ * first launch on a device; call it explicitly before capturing a stream into a hipGraph. */
+int come_init(int device);
+
+/* Host: the reference's EXP_TABLE (pyx:92-95,531-533), 1000 floats. Replaces the module-global
+ * table built by init() (pyx:512). */
+void come_exp_table(float *out1000);
+
+/* Host: value of the reference's FAST_VERSION (pyx:549).  Always 0: the dot product is consumed
+ * as float after a double-width reduction, like fast0_* (pyx:140). */
+int come_fast_version(void);
+
+/* ---- SGNS, second order (context over walks): replaces train_o2 (pyx:454-509) over a batch ----
+ * node, ctx   device fp32 [V x d] (node_embedding / context_embedding), updated in place.
+ * walks       device int32 [P x L] row indices; -1 (or any value outside [0,V)) = None; trailing
+ *             padding with -1 is equivalent to a shorter walk.  L <= 10000 (MAX_SENTENCE_LEN,
+ *             pyx:18,480).
+ * seeds       device uint64 [P], walk p's initial next_random (pyx:477: 2^24*randint+randint).
+ * table       device uint32 [T] negative-sampling table (model.py:97-122), values are rows.
+ * negative    0..20;  window >= 0;  1 <= d <= 512.
+ * The number of pair updates a batch performs is come_count_o2_pairs() of its walks.
+ */
+int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,
+                 int L, const uint64_t *seeds, int window, int negative, const uint32_t *table,
+                 uint64_t T, float lr, float alpha, int mode, void *stream);
+
+/* ---- SGNS, first order (edges): replaces train_o1 (pyx:407-450) over a batch ----
+ * edges       device int32 [E x 2] rows (u, v): pair (input u, positive v) then (input v,
+ *             positive u), RNG state carried across both (pyx:444-448).
+ * seeds       device uint64 [E], edge e's initial next_random (pyx:427). */
+int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
+                 const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T, float lr,
+                 int mode, void *stream);
+
+/* ---- Community gradient: replaces Community2Vec.train (community_embeddings.py:61-78) ----
+ * x [V x d] updated in place, `iters` times:
+ *   x_i -= lr * clip((beta/K) * sum_k pi[i,k] * inv_cov[k] @ (x_i - mu[k]), -5, 5)
+ * pi [V x K], mu [K x d], inv_cov [K x d x d] (all device fp32).  d % 32 == 0 or d <= 32. */
+int come_community_grad(float *x, int64_t V, int d, const float *pi, const float *mu,
+                        const float *inv_cov, int K, float beta, float lr, int iters,
+                        void *stream);
+
+/* ---- GMM responsibilities: replaces GaussianMixture.predict_proba (community_embeddings.py:37)
+ * for covariance_type='full'.  prec_chol [K x d x d] (precision Cholesky factors, sklearn
+ * layout), mu_prec [K x d] = mu_k @ prec_chol_k, log_norm [K] = log w_k + log det(prec_chol_k)
+ * - d/2 log(2 pi) (all device fp32, precomputed on the host from the fitted parameters).
+ * resp_out [V x K] device fp32.  K <= 64. */
+int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
+                  const float *log_norm, int K, float *resp_out, void *stream);
+
+/* ---- Host helpers ---- */
+
+/* Model.make_table (model.py:97-122), exact: same double accumulation, same start at node id 1,
+ * same clamp.  counts_by_id[0..V] (index 0 unused), table[T] (host memory).  O(V + T). */
+int come_make_table(const double *counts_by_id, int64_t V, uint32_t *table, uint64_t T,
+                    double power);
+
+/* Number of pair updates train_o2 performs on host walks [P x L] (-1 = None). */
+int64_t come_count_o2_pairs(const int32_t *walks, int64_t P, int L, int window);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* COME_H_ */

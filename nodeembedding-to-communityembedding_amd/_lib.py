@@ -1,0 +1,77 @@
+"""ctypes binding of libcome.so (the C-ABI in include/come.h).
+
+The HIP library is the only compute path: if it is missing or fails to load, every entry point
+raises -- there is no CPU fallback on the product path.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcome.so")
+
+MODE_HOGWILD = 0
+MODE_SEQUENTIAL = 1
+
+# Every symbol include/come.h declares (checked by tests/test_capi.py).
+SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
+           "come_fast_version", "come_sgns_o2", "come_sgns_o1", "come_community_grad",
+           "come_gmm_resp", "come_make_table", "come_count_o2_pairs")
+
+_lib = None
+
+
+class ComeError(RuntimeError):
+    pass
+
+
+def build():
+    """Compile libcome.so in-tree with hipcc (gfx950)."""
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "csrc"), "-j4"])
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ComeError("libcome.so not found at %s -- build it with "
+                        "`make -C nodeembedding-to-communityembedding_amd/csrc` or "
+                        "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, i64, u64, f32, f64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
+                                  ctypes.c_float, ctypes.c_double)
+    L.come_abi_version.restype = i32
+    L.come_last_error.restype = ctypes.c_char_p
+    L.come_init.argtypes = [i32]
+    L.come_exp_table.argtypes = [P]
+    L.come_exp_table.restype = None
+    L.come_sgns_o2.argtypes = [P, P, i64, i32, P, i64, i32, P, i32, i32, P, u64, f32, f32, i32, P]
+    L.come_sgns_o1.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, P]
+    L.come_community_grad.argtypes = [P, i64, i32, P, P, P, i32, f32, f32, i32, P]
+    L.come_gmm_resp.argtypes = [P, i64, i32, P, P, P, i32, P, P]
+    L.come_make_table.argtypes = [P, i64, P, u64, f64]
+    L.come_count_o2_pairs.argtypes = [P, i64, i32, i32]
+    L.come_count_o2_pairs.restype = i64
+    if L.come_abi_version() != 1:
+        raise ComeError("libcome.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().come_last_error().decode(errors="replace")
+        raise ComeError("%s failed (rc=%d): %s" % (what, rc, msg))
+
+
+def ptr(t):
+    """Raw address of a torch tensor or numpy array (no torch types cross the C-ABI)."""
+    if hasattr(t, "data_ptr"):
+        return ctypes.c_void_p(t.data_ptr())
+    return t.ctypes.data_as(ctypes.c_void_p)
+
+
+def stream_handle(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

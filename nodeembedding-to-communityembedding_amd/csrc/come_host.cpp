@@ -1,0 +1,150 @@
+// come_host.cpp -- host side of libcome.so: error reporting, per-device init, the reference's
+// EXP_TABLE, the exact make_table, pair counting.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "come_internal.h"
+
+extern "C" int come_upload_exp_table(const float *host1000);  // come_sgns.hip
+
+namespace come {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_error(hipError_t e, const char *what) {
+    if (e == hipSuccess) return COME_OK;
+    return set_error(COME_E_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+static constexpr int kMaxDevices = 64;
+static std::once_flag g_once[kMaxDevices];
+static int g_init_rc[kMaxDevices];
+static int g_cus[kMaxDevices];
+
+static void init_device(int dev) {
+    float tab[kExpTableSize];
+    come_exp_table(tab);
+    g_init_rc[dev] = come_upload_exp_table(tab);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) g_cus[dev] = prop.multiProcessorCount;
+    if (g_cus[dev] <= 0) g_cus[dev] = 256;
+}
+
+int ensure_init(int *device_out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_error(e, "hipGetDevice");
+    if (dev < 0 || dev >= kMaxDevices) return set_error(COME_E_UNSUPPORTED, "device %d", dev);
+    std::call_once(g_once[dev], init_device, dev);
+    if (device_out) *device_out = dev;
+    if (g_init_rc[dev]) return set_error(g_init_rc[dev], "come_init failed on device %d", dev);
+    return COME_OK;
+}
+
+int num_cus(int device) { return g_cus[device] > 0 ? g_cus[device] : 256; }
+
+}  // namespace come
+
+using namespace come;
+
+extern "C" int come_abi_version(void) { return COME_ABI_VERSION; }
+
+extern "C" const char *come_last_error(void) { return g_err; }
+
+extern "C" int come_fast_version(void) { return 0; }
+
+extern "C" int come_init(int device) {
+    int cur = 0;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return hip_error(e, "hipGetDevice");
+    if (device != cur) {
+        e = hipSetDevice(device);
+        if (e != hipSuccess) return hip_error(e, "hipSetDevice");
+    }
+    int rc = ensure_init(nullptr);
+    if (device != cur) (void)hipSetDevice(cur);
+    return rc;
+}
+
+// pyx:531-533, with the promotions of the generated C: i/(float)1000 in float, the rest in double,
+// stored as float twice.
+extern "C" void come_exp_table(float *out) {
+    for (int i = 0; i < kExpTableSize; ++i) {
+        const float q = (float)i / (float)kExpTableSize;
+        const float e = (float)exp(((double)q * 2.0 - 1.0) * 6.0);
+        out[i] = (float)((double)e / ((double)e + 1.0));
+    }
+}
+
+// model.py:97-122.  The literal loop is O(T) with one double division per slot; here each run of
+// equal values is located directly: the slot where `widx` advances is the first t >= pos with
+// (double)t / T > d1 (the predicate is monotone in t), found from floor(d1 * T) and corrected by
+// exact re-evaluation of the reference's own predicate, so the output is identical slot for slot.
+extern "C" int come_make_table(const double *counts_by_id, int64_t V, uint32_t *table, uint64_t T,
+                               double power) {
+    if (!counts_by_id || !table) return set_error(COME_E_INVALID, "null pointer");
+    if (V < 2) return set_error(COME_E_INVALID, "make_table needs V >= 2 (got %lld)", (long long)V);
+    if (T == 0) return COME_OK;
+    double z = 0.0;
+    for (int64_t id = 1; id <= V; ++id) z += pow(counts_by_id[id], power);
+    const double Td = (double)T;
+    auto pred = [&](uint64_t t, double d1) { return 1.0 * (double)t / Td > d1; };
+    int64_t widx = 1;
+    double d1 = pow(counts_by_id[1], power) / z;
+    uint64_t pos = 0;
+    while (pos < T) {
+        // first t >= pos at which the reference advances widx (stores widx at t, then advances)
+        uint64_t t;
+        if (pred(pos, d1)) {
+            t = pos;
+        } else {
+            double guess = floor(d1 * Td);
+            uint64_t c = guess < (double)pos ? pos : (guess >= Td ? T : (uint64_t)guess);
+            while (c > pos && pred(c - 1, d1)) --c;
+            while (c < T && !pred(c, d1)) ++c;
+            t = c;  // may be T: no further advance
+        }
+        const uint64_t end = t < T ? t + 1 : T;  // slots [pos, end) hold widx
+        for (uint64_t s = pos; s < end; ++s) table[s] = (uint32_t)widx;
+        pos = end;
+        if (t >= T) break;
+        widx += 1;
+        d1 += pow(counts_by_id[widx], power) / z;
+        if (widx >= V) {  // clamp (model.py:120-121): every later slot holds V-1
+            for (uint64_t s = pos; s < T; ++s) table[s] = (uint32_t)(V - 1);
+            break;
+        }
+    }
+    return COME_OK;
+}
+
+// train_o2's loop nest (pyx:494-506) without the work: one count per fast_o2 call.
+extern "C" int64_t come_count_o2_pairs(const int32_t *walks, int64_t P, int L, int window) {
+    if (!walks || P <= 0 || L <= 0 || window < 0) return 0;
+    const int path_len = L < kMaxSentenceLen ? L : kMaxSentenceLen;
+    int64_t total = 0;
+    for (int64_t p = 0; p < P; ++p) {
+        const int32_t *idx = walks + p * (int64_t)L;
+        for (int i = 0; i < path_len; ++i) {
+            if (idx[i] < 0) continue;
+            const int j0 = i - window < 0 ? 0 : i - window;
+            const int j1 = i + window + 1 > path_len ? path_len : i + window + 1;
+            for (int j = j0; j < j1; ++j)
+                if (j != i && idx[j] >= 0) ++total;
+        }
+    }
+    return total;
+}

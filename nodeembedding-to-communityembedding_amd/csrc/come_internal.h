@@ -1,0 +1,43 @@
+// Internal helpers shared by the libcome.so translation units (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/come.h"
+
+namespace come {
+
+// The reference's compile-time constants (pyx:18,92-93,121,134).
+constexpr int kExpTableSize = 1000;
+constexpr int kMaxExp = 6;
+constexpr int kMaxSentenceLen = 10000;
+constexpr uint64_t kLcgMul = 25214903917ULL;
+constexpr uint64_t kLcgAdd = 11ULL;
+constexpr uint64_t kLcgMask = (1ULL << 48) - 1;
+constexpr int kMaxNegative = 20;
+constexpr int kMaxDim = 512;
+
+int set_error(int code, const char *fmt, ...);  // returns code
+int hip_error(hipError_t e, const char *what);  // returns COME_E_HIP (or OK if e == success)
+int ensure_init(int *device_out);               // come_init() for the current device, once
+int num_cus(int device);                        // multiprocessor count (cached)
+
+// Lemire fastmod: a % d for 32-bit a, d >= 1, from one 64-bit multiply-high.  m = 0 encodes
+// "d >= 2^32" (then a % d == a for every 32-bit a).
+struct FastMod {
+    uint64_t m;
+    uint32_t d;
+};
+inline FastMod make_fastmod(uint64_t T) {
+    FastMod f;
+    if (T >= (1ULL << 32)) {
+        f.m = 0;
+        f.d = 0;
+    } else {
+        f.d = (uint32_t)T;
+        f.m = UINT64_C(0xFFFFFFFFFFFFFFFF) / f.d + 1;  // d == 1 -> m == 0 -> result 0 (correct)
+    }
+    return f;
+}
+
+}  // namespace come

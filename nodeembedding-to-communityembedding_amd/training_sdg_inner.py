@@ -1,0 +1,185 @@
+"""Drop-in for the reference's Cython module ``utils/training_sdg_inner.pyx``.
+
+Same names and argument meaning as the reference:
+
+    train_o1(py_node_embedding, py_edge, py_lr, py_negative, py_table, py_size=None, py_work=None)
+        -> int                                                          (pyx:407-450)
+    train_o2(py_node_embedding, py_context_embedding, py_path, py_lr, py_negative, py_window,
+             py_table, py_alpha=1.0, py_size=None, py_work=None) -> int (pyx:454-509)
+    init() -> int, FAST_VERSION                                         (pyx:512-549)
+
+Like the reference they mutate the embedding tables IN PLACE and draw each call's initial
+``next_random`` from the global numpy RNG (2 draws, pyx:427,477).  The tables may be CUDA
+tensors (the fast, intended path: no copies) or numpy arrays (compatibility: copied to the GPU and
+back per call).  ``py_size`` and ``py_work`` are accepted and ignored (the kernel keeps its work
+vector in registers).
+
+The batched entry points ``sgns_o2`` / ``sgns_o1`` take whole batches of walks / edges already on
+the device and are what the trainers (Context2Vec / Node2Vec) call: one launch per batch instead
+of one Python call per walk.
+"""
+import numpy as np
+
+from . import _lib
+from ._lib import MODE_HOGWILD, MODE_SEQUENTIAL, check, ptr, stream_handle
+
+FAST_VERSION = 0
+MAX_SENTENCE_LEN = 10000
+
+
+def init():
+    """Returns FAST_VERSION (pyx:512-549).  The sigmoid table is uploaded per device by the
+    library on first use (come_init)."""
+    return _lib.lib().come_fast_version()
+
+
+def exp_table():
+    """The reference's EXP_TABLE (pyx:531-533) as a float32 numpy array of 1000 entries."""
+    out = np.zeros(1000, np.float32)
+    _lib.lib().come_exp_table(ptr(out))
+    return out
+
+
+def draw_seeds(n):
+    """Initial next_random of n consecutive train_o1/train_o2 calls, drawn from the global numpy
+    RNG exactly as pyx:427/477 does per call: 2^24 * randint(0, 2^24) + randint(0, 2^24)."""
+    n = int(n)
+    if n == 0:
+        return np.zeros(0, np.uint64)
+    ab = np.random.randint(0, 2 ** 24, size=2 * n).astype(np.uint64)
+    return (ab[0::2] << np.uint64(24)) + ab[1::2]
+
+
+def _require_cuda(t, name, dtype):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError("%s must be a CUDA tensor" % name)
+    if t.dtype != dtype:
+        raise TypeError("%s must be %s (got %s)" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+
+
+def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mode=MODE_HOGWILD):
+    """Batched train_o2: every walk of ``walks`` [P, L] (int32 rows, -1 = None) in one launch.
+
+    node, ctx: float32 CUDA tensors [V, d], updated in place.  seeds: uint64 (stored as int64)
+    CUDA tensor [P].  table: uint32 (stored as int32) CUDA tensor [T].  mode: MODE_HOGWILD (all
+    walks in flight, one wavefront each) or MODE_SEQUENTIAL (walks in order: workers=1)."""
+    import torch
+    _require_cuda(node, "node", torch.float32)
+    _require_cuda(ctx, "ctx", torch.float32)
+    _require_cuda(walks, "walks", torch.int32)
+    _require_cuda(seeds, "seeds", torch.int64)
+    _require_cuda(table, "table", torch.int32)
+    if node.shape != ctx.shape or node.dim() != 2:
+        raise ValueError("node and ctx must both be [V, d]")
+    if walks.dim() != 2 or seeds.shape != (walks.shape[0],):
+        raise ValueError("walks must be [P, L] and seeds [P]")
+    if walks.shape[1] > MAX_SENTENCE_LEN:  # pyx:480 truncates silently; so do we
+        walks = walks[:, :MAX_SENTENCE_LEN].contiguous()
+    V, d = node.shape
+    rc = _lib.lib().come_sgns_o2(ptr(node), ptr(ctx), V, d, ptr(walks), walks.shape[0],
+                                 walks.shape[1], ptr(seeds), int(window), int(negative),
+                                 ptr(table), table.numel(), float(lr), float(alpha), int(mode),
+                                 stream_handle(node.device))
+    check(rc, "come_sgns_o2")
+
+
+def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD):
+    """Batched train_o1 over ``edges`` [E, 2] (int32 rows) in one launch; node updated in place."""
+    import torch
+    _require_cuda(node, "node", torch.float32)
+    _require_cuda(edges, "edges", torch.int32)
+    _require_cuda(seeds, "seeds", torch.int64)
+    _require_cuda(table, "table", torch.int32)
+    if edges.dim() != 2 or edges.shape[1] != 2 or seeds.shape != (edges.shape[0],):
+        raise ValueError("edges must be [E, 2] and seeds [E]")
+    V, d = node.shape
+    rc = _lib.lib().come_sgns_o1(ptr(node), V, d, ptr(edges), edges.shape[0], ptr(seeds),
+                                 int(negative), ptr(table), table.numel(), float(lr), int(mode),
+                                 stream_handle(node.device))
+    check(rc, "come_sgns_o1")
+
+
+def count_o2_pairs(walks_np, window):
+    """Number of pair updates (fast_o2 calls) train_o2 makes over host walks [P, L]."""
+    w = np.ascontiguousarray(walks_np, np.int32)
+    if w.ndim != 2 or w.size == 0:
+        return 0
+    return int(_lib.lib().come_count_o2_pairs(ptr(w), w.shape[0], w.shape[1], int(window)))
+
+
+# ---- per-call drop-ins (reference signatures) -------------------------------------------------
+
+def _rows_of(items):
+    """Vocab objects (or None) -> int32 rows, -1 for None (codelens 0, pyx:483-490)."""
+    return np.array([-1 if it is None else int(it.index) for it in items], np.int32)
+
+
+class _DeviceTables:
+    """Resolve reference-style arguments (numpy or CUDA tensors) to CUDA tensors and write numpy
+    arguments back in place afterwards."""
+
+    def __init__(self, *arrays):
+        import torch
+        self.orig = arrays
+        self.dev = []
+        for a in arrays:
+            if isinstance(a, torch.Tensor):
+                if not a.is_cuda:
+                    raise TypeError("tables must be CUDA tensors or numpy arrays")
+                self.dev.append(a)
+            else:
+                self.dev.append(torch.from_numpy(np.ascontiguousarray(a)).cuda())
+
+    def writeback(self, *which):
+        import torch
+        for i in which:
+            if not isinstance(self.orig[i], torch.Tensor):
+                np.copyto(self.orig[i], self.dev[i].cpu().numpy())
+
+
+def _table_tensor(py_table):
+    import torch
+    if isinstance(py_table, torch.Tensor):
+        return py_table if py_table.dtype == torch.int32 else py_table.view(torch.int32)
+    return torch.from_numpy(np.ascontiguousarray(py_table, np.uint32).view(np.int32)).cuda()
+
+
+def train_o2(py_node_embedding, py_context_embedding, py_path, py_lr, py_negative, py_window,
+             py_table, py_alpha=1.0, py_size=None, py_work=None):
+    """One walk (pyx:454-509).  Returns the number of non-None entries."""
+    import torch
+    nr = int(draw_seeds(1)[0])  # pyx:477: two draws from the global numpy RNG, per call
+    items = list(py_path)[:MAX_SENTENCE_LEN]
+    rows = _rows_of(items)
+    result = int((rows >= 0).sum())
+    t = _DeviceTables(py_node_embedding, py_context_embedding)
+    dev = t.dev[0].device
+    walks = torch.from_numpy(rows.reshape(1, -1)).to(dev)
+    seeds = torch.tensor([nr], dtype=torch.int64).view(1).to(dev) if nr < 2 ** 63 else \
+        torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(dev)
+    if rows.size:
+        sgns_o2(t.dev[0], t.dev[1], walks, seeds, py_window, py_negative,
+                _table_tensor(py_table).to(dev), py_lr, py_alpha, MODE_SEQUENTIAL)
+    t.writeback(0, 1)
+    return result
+
+
+def train_o1(py_node_embedding, py_edge, py_lr, py_negative, py_table, py_size=None, py_work=None):
+    """One edge (pyx:407-450): pairs (edge[0] -> edge[1]) then (edge[1] -> edge[0]).  Returns the
+    number of non-None endpoints."""
+    import torch
+    nr = int(draw_seeds(1)[0])  # pyx:427
+    rows = _rows_of(list(py_edge)[:2])
+    result = int((rows >= 0).sum())
+    t = _DeviceTables(py_node_embedding)
+    dev = t.dev[0].device
+    if rows.size == 2:
+        edges = torch.from_numpy(rows.reshape(1, 2)).to(dev)
+        seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(dev)
+        sgns_o1(t.dev[0], edges, seeds, py_negative, _table_tensor(py_table).to(dev), py_lr,
+                MODE_SEQUENTIAL)
+    t.writeback(0)
+    return result

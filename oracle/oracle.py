@@ -1,0 +1,163 @@
+"""Python face of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and
+only as the checker.  The product package (come_amd) never imports it.
+
+* SGNS O1/O2 and make_table: ctypes over liboracle_come.so (come_oracle.c), a sequential C
+  restatement of utils/training_sdg_inner.pyx:105-509 and ADSCModel/model.py:97-122.
+* Community gradient: numpy restatement of ADSCModel/community_embeddings.py:61-78 (same fp32
+  numpy operations, same order).
+* GMM responsibilities: numpy restatement (float64) of what GaussianMixture.predict_proba does
+  for covariance_type='full' (sklearn 1.7.2 `_estimate_log_gaussian_prob` +
+  `_estimate_weighted_log_prob` + logsumexp normalisation), called by
+  community_embeddings.py:37, plus the fp32 np.linalg.inv of :36.
+
+Parity pin: tests/test_oracle_golden.py checks every function here against the fixtures that
+tests/golden/make_golden.py produced from the reference itself.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle_come.so")
+DOT_REF, DOT_WAVE64 = 0, 1
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE, "liboracle_come.so"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(
+                os.path.join(HERE, "come_oracle.c")):
+            build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        i64, u64, i32, f32, f64 = (ctypes.c_int64, ctypes.c_uint64, ctypes.c_int, ctypes.c_float,
+                                   ctypes.c_double)
+        L.oracle_exp_table.argtypes = [P]
+        L.oracle_lcg_next.argtypes = [u64]
+        L.oracle_lcg_next.restype = u64
+        L.oracle_sgns_o2.argtypes = [P, P, i32, P, i64, i32, P, i32, i32, P, u64, f32, f32, i32]
+        L.oracle_sgns_o2.restype = i64
+        L.oracle_sgns_o1.argtypes = [P, i32, P, i64, P, i32, P, u64, f32, i32]
+        L.oracle_sgns_o1.restype = i64
+        L.oracle_make_table.argtypes = [P, i64, P, u64, f64]
+        L.oracle_min_margin.restype = f64
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _chk(a, dt):
+    assert a.dtype == dt and a.flags.c_contiguous, (a.dtype, dt)
+    return a
+
+
+def exp_table():
+    out = np.zeros(1000, np.float32)
+    lib().oracle_exp_table(_p(out))
+    return out
+
+
+def lcg_next(s):
+    return int(lib().oracle_lcg_next(int(s)))
+
+
+def reset_margin():
+    lib().oracle_reset_margin()
+
+
+def min_margin():
+    return float(lib().oracle_min_margin())
+
+
+def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha, dot_mode=DOT_REF):
+    """In-place train_o2 over every walk in order (sequential, workers=1 semantics)."""
+    _chk(node, np.float32), _chk(ctx, np.float32), _chk(table, np.uint32)
+    walks = np.ascontiguousarray(walks, np.int32)
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    assert node.shape == ctx.shape and walks.shape[0] == seeds.shape[0]
+    return int(lib().oracle_sgns_o2(_p(node), _p(ctx), node.shape[1], _p(walks), walks.shape[0],
+                                    walks.shape[1], _p(seeds), window, negative, _p(table),
+                                    table.shape[0], lr, alpha, dot_mode))
+
+
+def sgns_o1(node, edges, seeds, negative, table, lr, dot_mode=DOT_REF):
+    """In-place train_o1 over every edge in order."""
+    _chk(node, np.float32), _chk(table, np.uint32)
+    edges = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    return int(lib().oracle_sgns_o1(_p(node), node.shape[1], _p(edges), edges.shape[0],
+                                    _p(seeds), negative, _p(table), table.shape[0], lr, dot_mode))
+
+
+def make_table(counts_by_row, T, power=0.75):
+    """counts_by_row[r] = count of node id r+1 (ids 1..V, model.py:66)."""
+    V = len(counts_by_row)
+    c = np.zeros(V + 1, np.float64)
+    c[1:] = counts_by_row
+    out = np.zeros(int(T), np.uint32)
+    lib().oracle_make_table(_p(c), V, _p(out), int(T), power)
+    return out
+
+
+def community_train(x, pi, mu, inv, beta, lr, iters, chunksize=150):
+    """community_embeddings.py:61-78 restated over all rows (nodes = every vocab entry)."""
+    x = x.copy()
+    V, K = pi.shape
+    idx_all = np.arange(V)
+    for _ in range(iters):
+        grad = np.zeros(x.shape, np.float32)
+        for s in range(0, V, chunksize):
+            ni = idx_all[s:s + chunksize]
+            inp = x[ni]
+            bg = np.zeros(inp.shape, np.float32)
+            for k in range(K):
+                diff = np.expand_dims(inp - mu[k], axis=-1)
+                m = pi[ni, k].reshape(len(ni), 1, 1) * inv[k]
+                bg += np.squeeze(np.matmul(m, diff), axis=-1)
+            grad[ni] += bg
+        grad *= (beta / K)
+        x -= grad.clip(min=-5, max=5) * lr
+    return x
+
+
+def precision_cholesky(cov):
+    """sklearn _compute_precision_cholesky('full') in float64."""
+    K, d, _ = cov.shape
+    out = np.empty((K, d, d))
+    for k in range(K):
+        c = np.linalg.cholesky(cov[k])
+        out[k] = np.linalg.solve(c, np.eye(d)).T  # == solve_triangular(c, I, lower=True).T
+    return out
+
+
+def gmm_log_resp(X, weights, means, cov):
+    """log responsibilities (V x K) of a full-covariance GMM, float64."""
+    X = np.asarray(X, np.float64)
+    pc = precision_cholesky(np.asarray(cov, np.float64))
+    K, d = means.shape
+    log_det = np.array([np.sum(np.log(np.diag(pc[k]))) for k in range(K)])
+    lp = np.empty((X.shape[0], K))
+    for k in range(K):
+        y = X @ pc[k] - means[k] @ pc[k]
+        lp[:, k] = np.sum(np.square(y), axis=1)
+    lp = -0.5 * (d * np.log(2 * np.pi) + lp) + log_det + np.log(weights)
+    m = lp.max(axis=1, keepdims=True)
+    lse = m + np.log(np.exp(lp - m).sum(axis=1, keepdims=True))
+    return lp - lse
+
+
+def gmm_predict_proba(X, weights, means, cov):
+    return np.exp(gmm_log_resp(X, weights, means, cov))

@@ -1,0 +1,59 @@
+"""The C-ABI library loads here (no GPU) and exports every symbol include/come.h declares;
+argument validation fails with an error code + message before any device work."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from come_amd import _lib
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "come.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\s*\*?\s*(come_[a-z0-9_]+)\(",
+                                 src, re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_symbols()
+    assert set(names) == set(_lib.SYMBOLS), names
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_symbols():
+        assert hasattr(L, name), name
+    assert L.come_abi_version() == 1
+
+
+def test_invalid_arguments_return_error_without_gpu():
+    L = _lib.lib()
+    p = ctypes.c_void_p(0)
+    rc = L.come_sgns_o2(p, p, 0, 128, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p)
+    assert rc == -1 and b"V must be" in L.come_last_error()
+    rc = L.come_sgns_o2(p, p, 10, 1000, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p)
+    assert rc == -1 and b"d must be" in L.come_last_error()
+    rc = L.come_sgns_o1(p, 10, 8, p, 1, p, 50, p, 10, 0.1, 0, p)
+    assert rc == -1 and b"negative" in L.come_last_error()
+    rc = L.come_sgns_o2(p, p, 10, 8, p, 1, 10, p, 5, 0, p, 10, 0.1, 1.0, 7, p)
+    assert rc == -1 and b"mode" in L.come_last_error()
+    # empty batches are a no-op (no device access)
+    assert L.come_sgns_o2(p, p, 10, 8, p, 0, 10, p, 5, 0, p, 10, 0.1, 1.0, 0, p) == 0
+    assert L.come_sgns_o1(p, 10, 8, p, 0, p, 0, p, 10, 0.1, 0, p) == 0
+
+
+def test_check_raises_with_message():
+    L = _lib.lib()
+    p = ctypes.c_void_p(0)
+    with pytest.raises(_lib.ComeError, match="V must be"):
+        _lib.check(L.come_sgns_o2(p, p, -1, 8, p, 1, 1, p, 1, 1, p, 1, 0.1, 1.0, 0, p), "o2")
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libcome.so")
+    with pytest.raises(_lib.ComeError, match="not found"):
+        _lib.lib()

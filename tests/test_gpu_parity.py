@@ -1,0 +1,318 @@
+"""GPU parity through the C-ABI (libcome.so on cuda:0).
+
+Bars (written per test):
+  * COME_MODE_SEQUENTIAL vs the oracle in its WAVE64 dot order: BIT-EXACT (same arithmetic in the
+    same order).
+  * vs the reference's golden vectors (tests/golden, produced by the Cython module itself):
+    tier A <= 1e-6 abs for clean cases, tier B <= 1e-3 abs where a dot product lies within 1e-4
+    bucket units of a sigmoid-table edge (OpenBLAS summation order can flip a bucket).
+  * COME_MODE_HOGWILD (many walks in flight, races like the reference's threads): statistical --
+    rows never touched stay bit-identical, the SGNS loss on held-out pairs within 1% of the
+    sequential run's.
+  * community gradient / GMM responsibilities (fp32 contractions in a different summation
+    order): rtol 1e-5 / atol 1e-5 vs the reference's numpy/sklearn outputs.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import oracle as orc
+
+import come_amd.training_sdg_inner as tsi
+from come_amd import community_embeddings as ce
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+KAT_O2 = np.load(os.path.join(GOLDEN, "kat_o2.npz"))
+KAT_O1 = np.load(os.path.join(GOLDEN, "kat_o1.npz"))
+
+
+def dev(a, dtype=None):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).to(DEV)
+
+
+def run_o2(node0, ctx0, walks, seeds, w, neg, table, lr, alpha, mode=tsi.MODE_SEQUENTIAL):
+    node, ctx = dev(node0.copy()), dev(ctx0.copy())
+    tsi.sgns_o2(node, ctx, dev(walks.astype(np.int32)), dev(seeds.astype(np.uint64)), w, neg,
+                dev(table), lr, alpha, mode)
+    torch.cuda.synchronize()
+    return node.cpu().numpy(), ctx.cpu().numpy()
+
+
+def run_o1(node0, edges, seeds, neg, table, lr, mode=tsi.MODE_SEQUENTIAL):
+    node = dev(node0.copy())
+    tsi.sgns_o1(node, dev(edges.astype(np.int32)), dev(seeds.astype(np.uint64)), neg, dev(table),
+                lr, mode)
+    torch.cuda.synchronize()
+    return node.cpu().numpy()
+
+
+def tol_for(margin):
+    return 1e-6 if margin >= 1e-4 else 1e-3
+
+
+# ---- O2 ----------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("name", list(KAT_O2["names"]))
+def test_o2_kat_bit_exact_vs_oracle_and_golden(name):
+    z, pre = KAT_O2, "o2_%s_" % name
+    d, neg, w, V, L, P = [int(x) for x in z[pre + "params"]]
+    lr, alpha = [float(x) for x in z[pre + "lr_alpha"]]
+    node, ctx = run_o2(z[pre + "node0"], z[pre + "ctx0"], z[pre + "walks"], z[pre + "seeds"], w,
+                       neg, z[pre + "table"], lr, alpha)
+    n_ref, c_ref = z[pre + "node0"].copy(), z[pre + "ctx0"].copy()
+    orc.sgns_o2(n_ref, c_ref, z[pre + "walks"], z[pre + "seeds"], w, neg, z[pre + "table"], lr,
+                alpha, dot_mode=orc.DOT_WAVE64)
+    np.testing.assert_array_equal(node, n_ref)
+    np.testing.assert_array_equal(ctx, c_ref)
+    tol = tol_for(float(z[pre + "margin"]))
+    np.testing.assert_allclose(node, z[pre + "node1"], rtol=0, atol=tol)
+    np.testing.assert_allclose(ctx, z[pre + "ctx1"], rtol=0, atol=tol)
+
+
+@pytest.mark.parametrize("d,neg,w,V,L,P,T", [
+    (128, 5, 5, 2000, 80, 24, 100000),   # the headline shape
+    (128, 10, 5, 40, 30, 8, 3000),       # small V: many repeated negatives / positive hits
+    (256, 10, 5, 500, 40, 6, 20000),
+    (512, 3, 2, 300, 20, 4, 5000),
+    (64, 5, 3, 100, 25, 10, 4000),
+    (96, 7, 4, 100, 25, 6, 4000),        # masked layout, MAXN = 10
+    (2, 4, 3, 34, 20, 20, 5000),         # Karate shape
+    (33, 15, 6, 80, 30, 5, 3000),        # MAXN = 20
+    (128, 0, 5, 100, 20, 5, 100),        # no negatives
+    (128, 5, 0, 100, 20, 5, 1000),       # window 0: no pairs, tables untouched
+    (128, 20, 1, 3, 10, 3, 100),         # V = 3: nearly every draw repeats
+])
+def test_o2_random_bit_exact_vs_oracle(d, neg, w, V, L, P, T):
+    rng = np.random.RandomState(d * 1000 + neg * 10 + V)
+    counts = rng.randint(1, 100, V)
+    table = orc.make_table(counts, T)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.2, 0.2, (V, d)).astype(np.float32)
+    walks = rng.randint(0, V, (P, L)).astype(np.int32)
+    walks[rng.uniform(size=walks.shape) < 0.05] = -1
+    seeds = rng.randint(0, 2 ** 48, P, dtype=np.int64).astype(np.uint64)
+    node, ctx = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.05, 0.9)
+    n_ref, c_ref = node0.copy(), ctx0.copy()
+    orc.sgns_o2(n_ref, c_ref, walks, seeds, w, neg, table, 0.05, 0.9, dot_mode=orc.DOT_WAVE64)
+    np.testing.assert_array_equal(node, n_ref)
+    np.testing.assert_array_equal(ctx, c_ref)
+    if w == 0:
+        np.testing.assert_array_equal(node, node0)
+
+
+def test_o2_out_of_range_rows_are_none():
+    """Walk entries >= V behave as None (never read/written); table values >= V are skipped."""
+    rng = np.random.RandomState(3)
+    V, d = 50, 128
+    table = orc.make_table(rng.randint(1, 9, V), 1000)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.1, 0.1, (V, d)).astype(np.float32)
+    walks = rng.randint(0, V, (4, 20)).astype(np.int32)
+    seeds = rng.randint(0, 2 ** 40, 4).astype(np.uint64)
+    bad = walks.copy()
+    bad[:, 5] = V + 7
+    ref_walks = walks.copy()
+    ref_walks[:, 5] = -1
+    a = run_o2(node0, ctx0, bad, seeds, 3, 5, table, 0.1, 1.0)
+    b = run_o2(node0, ctx0, ref_walks, seeds, 3, 5, table, 0.1, 1.0)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    bad_table = table.copy()
+    bad_table[::7] = V + 100  # never in range: those draws must be skipped, not read
+    run_o2(node0, ctx0, walks, seeds, 3, 5, bad_table, 0.1, 1.0)
+
+
+def test_o2_long_walk_truncated_at_max_sentence_len():
+    rng = np.random.RandomState(4)
+    V, d = 200, 64
+    table = orc.make_table(rng.randint(1, 9, V), 1000)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    walks = rng.randint(0, V, (1, 10050)).astype(np.int32)
+    seeds = np.array([123456789], np.uint64)
+    a = run_o2(node0, np.zeros_like(node0), walks, seeds, 2, 2, table, 0.01, 1.0)
+    b = run_o2(node0, np.zeros_like(node0), walks[:, :10000].copy(), seeds, 2, 2, table, 0.01,
+               1.0)
+    np.testing.assert_array_equal(a[0], b[0])
+
+
+def sgns_loss(node, ctx, walks, w, negatives):
+    """-sum log sigma over (input, positive) window pairs and fixed negative pairs."""
+    x, c = torch.from_numpy(node).double(), torch.from_numpy(ctx).double()
+    pairs = []
+    for walk in walks:
+        for i in range(len(walk)):
+            for j in range(max(0, i - w), min(len(walk), i + w + 1)):
+                if j != i:
+                    pairs.append((walk[j], walk[i]))
+    p = torch.tensor(pairs)
+    pos = (x[p[:, 0]] * c[p[:, 1]]).sum(1)
+    neg = (x[negatives[:, 0]] * c[negatives[:, 1]]).sum(1)
+    ls = torch.nn.functional.logsigmoid
+    return float(-(ls(pos).sum() + ls(-neg).sum()))
+
+
+def test_o2_hogwild_statistics():
+    """Many walks in flight: untouched rows stay identical; held-out loss within 1% of the
+    sequential (workers=1) run."""
+    rng = np.random.RandomState(5)
+    V, d, L, P, w, neg = 20000, 128, 40, 4000, 5, 5
+    counts = rng.randint(1, 50, V)
+    table = orc.make_table(counts, 200000)
+    node0 = rng.uniform(-0.5, 0.5, (V, d)).astype(np.float32) / 8
+    ctx0 = np.zeros((V, d), np.float32)
+    walks = rng.randint(0, V // 2, (P, L)).astype(np.int32)  # rows >= V/2 never an input
+    seeds = rng.randint(0, 2 ** 48, P, dtype=np.int64).astype(np.uint64)
+    hn, hc = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.025, 1.0, tsi.MODE_HOGWILD)
+    sn, sc = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.025, 1.0, tsi.MODE_SEQUENTIAL)
+    np.testing.assert_array_equal(hn[V // 2:], node0[V // 2:])
+    assert np.isfinite(hn).all() and np.isfinite(hc).all()
+    held = rng.randint(0, V // 2, (200, L))
+    negs = np.stack([rng.randint(0, V // 2, 5000), table[rng.randint(0, len(table), 5000)]], 1)
+    lh = sgns_loss(hn, hc, held, w, negs)
+    ls = sgns_loss(sn, sc, held, w, negs)
+    l0 = sgns_loss(node0, ctx0, held, w, negs)
+    assert lh < 0.95 * l0 and ls < 0.95 * l0
+    assert abs(lh - ls) / ls < 0.01, (lh, ls, l0)
+
+
+def test_o2_dropin_per_walk_numpy_and_tensor():
+    """train_o2 with the reference signature: numpy tables mutated in place, seeds from the global
+    numpy RNG, Vocab-like path items, return value = non-None count."""
+    z, pre = KAT_O2, "o2_d2_n4_w3_"
+    d, neg, w, V, L, P = [int(x) for x in z[pre + "params"]]
+    lr, alpha = [float(x) for x in z[pre + "lr_alpha"]]
+    node, ctx = z[pre + "node0"].copy(), z[pre + "ctx0"].copy()
+    tnode, tctx = dev(node.copy()), dev(ctx.copy())
+
+    class V_:
+        def __init__(self, i):
+            self.index = i
+    for p in range(P):
+        path = [V_(int(x)) if x >= 0 else None for x in z[pre + "walks"][p]]
+        np.random.seed(1000 * 0 + p)
+        r = tsi.train_o2(node, ctx, path, lr, neg, w, z[pre + "table"], py_alpha=alpha, py_size=d,
+                         py_work=np.zeros(d, np.float32))
+        assert r == z[pre + "ret"][p]
+        np.random.seed(1000 * 0 + p)
+        tsi.train_o2(tnode, tctx, path, lr, neg, w, dev(z[pre + "table"]), py_alpha=alpha)
+    np.testing.assert_allclose(node, z[pre + "node1"], atol=tol_for(float(z[pre + "margin"])))
+    np.testing.assert_allclose(ctx, z[pre + "ctx1"], atol=tol_for(float(z[pre + "margin"])))
+    np.testing.assert_array_equal(tnode.cpu().numpy(), node)
+
+
+# ---- O1 ----------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("name", list(KAT_O1["names"]))
+def test_o1_kat_bit_exact_vs_oracle_and_golden(name):
+    z, pre = KAT_O1, "o1_%s_" % name
+    d, neg, V, E = [int(x) for x in z[pre + "params"]]
+    lr = float(z[pre + "lr"][0])
+    node = run_o1(z[pre + "node0"], z[pre + "edges"], z[pre + "seeds"], neg, z[pre + "table"], lr)
+    n_ref = z[pre + "node0"].copy()
+    orc.sgns_o1(n_ref, z[pre + "edges"], z[pre + "seeds"], neg, z[pre + "table"], lr,
+                dot_mode=orc.DOT_WAVE64)
+    np.testing.assert_array_equal(node, n_ref)
+    np.testing.assert_allclose(node, z[pre + "node1"], rtol=0,
+                               atol=tol_for(float(z[pre + "margin"])))
+
+
+@pytest.mark.parametrize("d,neg,V,E", [(128, 5, 5000, 3000), (2, 4, 34, 78), (256, 10, 300, 500),
+                                       (100, 20, 50, 200), (128, 5, 3, 50), (512, 1, 100, 64)])
+def test_o1_random_bit_exact_vs_oracle(d, neg, V, E):
+    rng = np.random.RandomState(d + neg + V)
+    table = orc.make_table(rng.randint(1, 30, V), 5 * V + 7)
+    node0 = rng.uniform(-0.5, 0.5, (V, d)).astype(np.float32)
+    edges = rng.randint(0, V, (E, 2)).astype(np.int32)
+    edges[::17, 1] = edges[::17, 0]  # self loops
+    seeds = rng.randint(0, 2 ** 48, E, dtype=np.int64).astype(np.uint64)
+    node = run_o1(node0, edges, seeds, neg, table, 0.2)
+    n_ref = node0.copy()
+    orc.sgns_o1(n_ref, edges, seeds, neg, table, 0.2, dot_mode=orc.DOT_WAVE64)
+    np.testing.assert_array_equal(node, n_ref)
+
+
+def test_o1_dropin_per_edge():
+    z, pre = KAT_O1, "o1_d2_n4_"
+    d, neg, V, E = [int(x) for x in z[pre + "params"]]
+    node = z[pre + "node0"].copy()
+
+    class V_:
+        def __init__(self, i):
+            self.index = i
+    for e in range(E):
+        np.random.seed(50000 + e)
+        r = tsi.train_o1(node, [V_(int(z[pre + "edges"][e, 0])), V_(int(z[pre + "edges"][e, 1]))],
+                         float(z[pre + "lr"][0]), neg, z[pre + "table"], py_size=d)
+        assert r == 2
+    np.testing.assert_allclose(node, z[pre + "node1"], atol=tol_for(float(z[pre + "margin"])))
+
+
+# ---- community gradient / GMM responsibilities -------------------------------------------------
+
+def test_community_grad_vs_golden():
+    z = np.load(os.path.join(GOLDEN, "community.npz"))
+    for name in z["names"]:
+        p = name + "_"
+        beta, lr = [float(x) for x in z[p + "scal"]]
+        x = dev(z[p + "x0"])
+        ce.community_grad(x, dev(z[p + "pi"]), dev(z[p + "mu"]), dev(z[p + "inv"]), beta, lr,
+                          int(z[p + "iters"]))
+        np.testing.assert_allclose(x.cpu().numpy(), z[p + "x1"], rtol=1e-5, atol=1e-5,
+                                   err_msg=name)
+
+
+def test_gmm_resp_vs_golden():
+    z = np.load(os.path.join(GOLDEN, "gmm_resp.npz"))
+    for name in z["names"]:
+        p = name + "_"
+        pc = orc.precision_cholesky(z[p + "cov"])
+        args = ce.gmm_resp_params(z[p + "w"], z[p + "mu"], pc, DEV)
+        pi = ce.gmm_resp(dev(z[p + "X"]), *args).cpu().numpy()
+        np.testing.assert_allclose(pi, z[p + "pi"], rtol=0, atol=2e-5, err_msg=name)
+        np.testing.assert_allclose(pi.sum(1), 1.0, atol=1e-5)
+
+
+# ---- whole Karate flow (adsc_Karate.py:104-137, workers=1) -------------------------------------
+
+def test_karate_flow_deterministic():
+    from come_amd.community_embeddings import Community2Vec
+    from come_amd.context_embeddings import Context2Vec
+    from come_amd.model import Model
+    from come_amd.node_embeddings import Node2Vec
+    z = np.load(os.path.join(GOLDEN, "karate.npz"))
+    size, neg, ws, lr, alpha, beta, T = z["hyper"]
+    deg = dict(zip(z["degree_ids"].tolist(), z["degree_counts"].tolist()))
+    np.random.seed(42)
+    m = Model(deg, size=int(size), table_size=int(T), k=2)
+    np.testing.assert_array_equal(m.node_embedding.cpu().numpy(), z["node_init"])
+    nl = Node2Vec(workers=1, negative=int(neg), lr=float(lr), deterministic=True)
+    cl = Context2Vec(window_size=int(ws), workers=1, negative=int(neg), lr=float(lr),
+                     deterministic=True)
+    np.random.seed(100)
+    nl.train(m, edges=z["edges"], iter=1, chunksize=20)
+    np.testing.assert_allclose(m.node_embedding.cpu().numpy(), z["after_o1_pre"], atol=1e-3)
+    np.random.seed(101)
+    cl.train(m, paths=z["walks"], total_nodes=z["walks"].size, alpha=float(alpha), chunksize=20)
+    np.testing.assert_allclose(m.node_embedding.cpu().numpy(), z["after_o2_pre_node"], atol=1e-3)
+    np.testing.assert_allclose(m.context_embedding.cpu().numpy(), z["after_o2_pre_ctx"], atol=1e-3)
+    np.random.seed(102)
+    nl.train(m, edges=z["edges"], iter=1, chunksize=20)
+    np.random.seed(103)
+    cl.train(m, paths=z["walks"], total_nodes=z["walks"].size, alpha=float(alpha), chunksize=20)
+    np.testing.assert_allclose(m.node_embedding.cpu().numpy(), z["after_loop_node"], atol=1e-3)
+    # community step on the reference's own fitted GMM parameters
+    m.node_embedding.copy_(dev(z["after_loop_node"]))
+    m.centroid, m.inv_covariance_mat, m.pi = (dev(z["gmm_centroid"]), dev(z["gmm_inv"]),
+                                              dev(z["gmm_pi"]))
+    cm = Community2Vec(m, reg_covar=1e-5, lr=float(lr))
+    cm.train(list(range(1, 35)), m, float(beta), chunksize=20, iter=5)
+    np.testing.assert_allclose(m.node_embedding.cpu().numpy(), z["after_com_node"], atol=1e-5)

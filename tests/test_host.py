@@ -1,0 +1,175 @@
+"""Host-side logic of the product package (no GPU): the native make_table, pair counting, seed
+drawing, walk -> row conversion, Model construction, text IO, sharding."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import oracle as orc
+
+import come_amd.training_sdg_inner as tsi
+from come_amd import _lib, io_utils
+from come_amd.distributed import shard_range, shard_walks
+from come_amd.embedding import RepeatCorpusNTimes, chunkize_serial
+from come_amd.model import Model
+
+
+def native_make_table(counts_by_row, T, power=0.75):
+    c = np.zeros(len(counts_by_row) + 1, np.float64)
+    c[1:] = counts_by_row
+    out = np.zeros(int(T), np.uint32)
+    _lib.check(_lib.lib().come_make_table(_lib.ptr(c), len(counts_by_row), _lib.ptr(out), int(T),
+                                         power), "make_table")
+    return out
+
+
+@pytest.mark.parametrize("seed,V,T", [(0, 2, 10), (1, 3, 7), (2, 10, 1000), (3, 1000, 100000),
+                                      (4, 5000, 12345), (5, 50, 49), (6, 3000, 3000),
+                                      (7, 200, 1)])
+def test_native_make_table_equals_literal_loop(seed, V, T):
+    rng = np.random.RandomState(seed)
+    counts = np.maximum(1, (rng.pareto(1.2, V) * 5).astype(np.int64))
+    np.testing.assert_array_equal(native_make_table(counts, T), orc.make_table(counts, T))
+
+
+def test_native_make_table_golden():
+    import hashlib
+    z = np.load(os.path.join(GOLDEN, "make_table.npz"))
+    for name in z["names"]:
+        t = native_make_table(z[name + "_counts"], int(z[name + "_T"]))
+        if name + "_table" in z:
+            np.testing.assert_array_equal(t, z[name + "_table"])
+        else:
+            assert hashlib.sha256(t.tobytes()).hexdigest() == str(z[name + "_sha256"])
+
+
+def test_native_make_table_clamp_heavy_tail():
+    counts = np.array([1] * 5 + [10 ** 6])  # last id carries almost all mass -> clamp to V-1
+    np.testing.assert_array_equal(native_make_table(counts, 5000), orc.make_table(counts, 5000))
+
+
+def test_exp_table_native_equals_oracle():
+    np.testing.assert_array_equal(tsi.exp_table(), orc.exp_table())
+    assert tsi.init() == tsi.FAST_VERSION == 0
+
+
+def test_count_pairs():
+    rng = np.random.RandomState(0)
+    for L, w in [(80, 5), (20, 3), (3, 5), (1, 2), (10, 0)]:
+        walks = rng.randint(0, 50, (7, L)).astype(np.int32)
+        n = tsi.count_o2_pairs(walks, w)
+        if L >= w + 1:
+            assert n == 7 * (2 * w * L - w * (w + 1))
+        node = np.zeros((50, 4), np.float32)
+        ctx = np.zeros((50, 4), np.float32)
+        assert n == orc.sgns_o2(node, ctx, walks, np.zeros(7, np.uint64), w, 0,
+                                np.zeros(1, np.uint32), 0.1, 1.0)
+    walks[:, ::3] = -1
+    node = np.zeros((50, 4), np.float32)
+    assert tsi.count_o2_pairs(walks, 2) == orc.sgns_o2(
+        node, node.copy(), walks, np.zeros(7, np.uint64), 2, 0, np.zeros(1, np.uint32), 0.1, 1.0)
+
+
+def test_draw_seeds_matches_per_call_draws():
+    """pyx:427/477: two np.random.randint(0, 2**24) draws per call, in call order."""
+    np.random.seed(77)
+    fast = tsi.draw_seeds(1000)
+    np.random.seed(77)
+    slow = [(2 ** 24) * np.random.randint(0, 2 ** 24) + np.random.randint(0, 2 ** 24)
+            for _ in range(1000)]
+    np.testing.assert_array_equal(fast, np.array(slow, np.uint64))
+    assert (fast < 2 ** 48).all()
+
+
+def karate_model(**kw):
+    z = np.load(os.path.join(GOLDEN, "karate.npz"))
+    deg = dict(zip(z["degree_ids"].tolist(), z["degree_counts"].tolist()))
+    np.random.seed(42)
+    return Model(deg, size=2, table_size=int(z["hyper"][6]), k=2, device="cpu", **kw), z
+
+
+def test_model_matches_reference_init():
+    m, z = karate_model()
+    np.testing.assert_array_equal(m.node_embedding.numpy(), z["node_init"])
+    np.testing.assert_array_equal(np.bincount(m.table_host, minlength=34), z["table_bincount"])
+    assert m.vocab[1].index == 0 and m.vocab[34].index == 33
+    assert (m.context_embedding.numpy() == 0).all()
+    assert tuple(m.pi.shape) == (34, 2) and tuple(m.inv_covariance_mat.shape) == (2, 2, 2)
+
+
+def test_walks_to_rows_drops_oov_and_pads():
+    from come_amd.embedding import walks_to_rows
+    m, _ = karate_model()
+    rows = walks_to_rows(m, [[1, 2, 99, 3], [34], [0, 5]])
+    np.testing.assert_array_equal(rows, [[0, 1, 2], [33, -1, -1], [4, -1, -1]])
+    arr = np.array([[1, 2, 3], [4, 5, 6]])
+    np.testing.assert_array_equal(walks_to_rows(m, arr), arr - 1)
+
+
+def test_down_sampling_draw_count():
+    from come_amd.embedding import walks_to_rows
+    m, _ = karate_model(down_sampling=0.005)
+    p = m.sample_probability_rows()
+    walk = np.arange(1, 35)
+    low = int((p < 1).sum())
+    assert 0 < low < 34
+    np.random.seed(5)
+    walks_to_rows(m, [walk])
+    after = np.random.random_sample()
+    np.random.seed(5)
+    np.random.random_sample(low)
+    assert np.random.random_sample() == after
+
+
+def test_save_load_roundtrip(tmp_path):
+    m, _ = karate_model()
+    m.save(str(tmp_path), "karate")
+    m2 = Model.load_model(str(tmp_path), "karate", device="cpu")
+    np.testing.assert_array_equal(m2.node_embedding.numpy(), m.node_embedding.numpy())
+    np.testing.assert_array_equal(m2.table_host, m.table_host)
+    assert m2.vocab[34].index == 33
+
+
+def test_io_roundtrip(tmp_path):
+    x = np.random.RandomState(1).randn(5, 3).astype(np.float32)
+    io_utils.save_embedding(x, "e", path=str(tmp_path))
+    lines = open(os.path.join(str(tmp_path), "e.txt")).read().splitlines()
+    assert lines[0].split("\t")[0] == "1" and len(lines) == 5
+    np.testing.assert_allclose(io_utils.load_embedding("e", path=str(tmp_path)), x, rtol=1e-6)
+    io_utils.save_ground_true("lab", [1, 2, 2], path=str(tmp_path))
+    os.rename(os.path.join(str(tmp_path), "lab.txt"), os.path.join(str(tmp_path), "lab.labels"))
+    labels, k = io_utils.load_ground_true(path=str(tmp_path), file_name="lab")
+    assert labels == [1, 2, 2] and k == 2
+
+
+def test_chunkize_and_repeat():
+    assert list(chunkize_serial(range(10), 3)) == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9]]
+    assert list(RepeatCorpusNTimes([1, 2], 3)) == [1, 2, 1, 2, 1, 2]
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (7, 8), (0, 2), (100, 1), (1001, 8)])
+def test_shard_range_partitions(n, world):
+    seen = []
+    for r in range(world):
+        lo, hi = shard_range(n, r, world)
+        seen.extend(range(lo, hi))
+    assert seen == list(range(n))
+    w, s = shard_walks(np.arange(n * 2).reshape(n, 2), np.arange(n), world - 1, world)
+    assert len(w) == len(s)
+
+
+def test_graph_generators():
+    from come_amd.graph import CSRGraph, chung_lu, sbm
+    g = chung_lu(2000, 10, seed=1)
+    assert g.V == 2000 and g.num_edges > 5000
+    assert g.rowptr[-1] == 2 * g.num_edges and g.degree.max() > 5 * g.degree.mean()
+    s = sbm(4, 100, 0.1, 0.001, seed=0)
+    assert s.V == 400 and s.num_edges > 0
+    ids, deg = s.degree_by_id()
+    assert ids[0] == 1 and deg.sum() == 2 * s.num_edges
+    g2, ids = CSRGraph.from_adjlist(os.path.join(GOLDEN, "..", "..", "tests", "golden",
+                                                 "karate.adjlist")) \
+        if os.path.exists(os.path.join(GOLDEN, "karate.adjlist")) else (None, None)
+    if g2 is not None:
+        assert g2.V == 34 and g2.num_edges == 78
