@@ -1,0 +1,55 @@
+"""Summarise a scripts/profile.sh run into profiles/: the rocprofv3 kernel stats of the bench's
+dominant kernel, its per-launch HBM traffic from the PMC passes, and profiles/traffic.json (read
+by bench.py for roofline.traffic).
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
+FETCH_SIZE reports half the bytes of wide coalesced reads (128-B requests tallied at 64 B), so
+read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE * 1024 is exact for full-line stores.
+Usage: python scripts/summarize_profile.py gpurun_out/prof_r01 r01
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+KERNEL = "k_sgns_o2"
+
+
+def main(src, tag, kernel=KERNEL):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = os.path.join(root, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, "%s_kernel_stats.csv" % tag))
+    row = [r for r in csv.DictReader(open(stats)) if kernel in r["Name"]][0]
+    avg_ms = float(row["AverageNs"]) / 1e6
+    pmc = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = [r for r in csv.DictReader(open(os.path.join(src, "pmc_" + c,
+                                                            "run_counter_collection.csv")))
+                if kernel in r["Kernel_Name"]]
+        vals = [float(r["Counter_Value"]) for r in rows]
+        pmc[c] = sum(vals) / len(vals)
+        pmc[c + "_launches"] = len(vals)
+    read_b = 2 * pmc["FETCH_SIZE"] * 1024
+    write_b = pmc["WRITE_SIZE"] * 1024
+    bench = json.load(open(os.path.join(src, "trace_bench.json")))
+    cfg = bench["config"]
+    pairs = cfg["pairs_per_step_per_gpu"]
+    alg = bench["roofline"]["bytes_per_pair"] * pairs
+    traffic = {"kernel": row["Name"], "tag": tag, "walks_per_launch": cfg["walks_per_step_per_gpu"],
+               "dim": 128, "negative": 5, "hbm_bytes_per_launch": read_b + write_b,
+               "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
+               "algorithmic_bytes_per_launch": alg, "pairs_per_launch": pairs,
+               "rocprof_avg_kernel_ms": avg_ms,
+               "bench_event_avg_kernel_ms": bench["roofline"]["avg_kernel_ms"],
+               "actual_hbm_GBps": (read_b + write_b) / avg_ms / 1e6,
+               "raw": pmc}
+    json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    json.dump(traffic, open(os.path.join(dst, "%s_traffic.json" % tag), "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

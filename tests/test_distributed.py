@@ -1,0 +1,75 @@
+"""Multi-process (world size 2, gloo, CPU) tests of the walk sharding and the delta all-reduce
+that bench.py runs over RCCL on the GPU."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from come_amd.distributed import DeltaAllReduce, reference_delta_sum, shard_walks
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.RandomState(0)
+    w_sync = [rng.randn(37, 8).astype(np.float32), rng.randn(37, 8).astype(np.float32)]
+    tables = [torch.from_numpy(t.copy()) for t in w_sync]
+    sync = DeltaAllReduce(tables, bucket_elems=50)  # several buckets per table
+    # each rank makes its own local progress
+    local = []
+    for i, t in enumerate(tables):
+        delta = np.random.RandomState(100 + 10 * rank + i).randn(*t.shape).astype(np.float32)
+        t.add_(torch.from_numpy(delta))
+        local.append(t.numpy().copy())
+    sync.sync()
+    np.save(os.path.join(out_dir, "r%d_t0.npy" % rank), tables[0].numpy())
+    np.save(os.path.join(out_dir, "r%d_t1.npy" % rank), tables[1].numpy())
+    np.save(os.path.join(out_dir, "r%d_local0.npy" % rank), local[0])
+    np.save(os.path.join(out_dir, "r%d_local1.npy" % rank), local[1])
+    # second sync with no progress is a no-op
+    before = tables[0].clone()
+    sync.sync()
+    assert torch.equal(before, tables[0])
+    # sharding: every walk exactly once across ranks
+    walks = np.arange(101 * 3).reshape(101, 3)
+    seeds = np.arange(101)
+    ws, ss = shard_walks(walks, seeds, rank, world)
+    got = [None] * world
+    dist.all_gather_object(got, ss.tolist())
+    if rank == 0:
+        assert sorted(sum(got, [])) == list(range(101))
+    dist.destroy_process_group()
+
+
+def test_delta_allreduce_world2(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    rng = np.random.RandomState(0)
+    w_sync = [rng.randn(37, 8).astype(np.float32), rng.randn(37, 8).astype(np.float32)]
+    for i in range(2):
+        locals_ = [np.load(os.path.join(str(tmp_path), "r%d_local%d.npy" % (r, i)))
+                   for r in range(world)]
+        expect = reference_delta_sum(w_sync[i], locals_)
+        r0 = np.load(os.path.join(str(tmp_path), "r0_t%d.npy" % i))
+        r1 = np.load(os.path.join(str(tmp_path), "r1_t%d.npy" % i))
+        np.testing.assert_array_equal(r0, r1)          # replicas agree after a sync
+        np.testing.assert_allclose(r0, expect, rtol=0, atol=1e-5)
+
+
+def test_single_rank_sync_is_noop():
+    t = torch.randn(10, 4)
+    before = t.clone()
+    DeltaAllReduce([t]).sync()
+    assert torch.equal(t, before)
