@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+KERNEL = "come::k_sgns_o2_ring<2, true, 5, true>"  # the launch bench.py times (d=128, n=5, Hogwild)
 
 
 def log(*a):
@@ -226,7 +227,8 @@ def main():
         try:
             tj = json.load(open(args.traffic_json))
             if (tj.get("walks_per_launch") == B and tj.get("dim") == d
-                    and tj.get("negative") == n):
+                    and tj.get("negative") == n
+                    and KERNEL.replace(" ", "") in tj.get("kernel", "").replace(" ", "")):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -284,7 +286,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "come::k_sgns_o2<2,true,5>",
+            "kernel": KERNEL,
             "bytes_per_pair": bytes_per_pair,
             "avg_kernel_ms": avg_kernel_s * 1e3,
         },

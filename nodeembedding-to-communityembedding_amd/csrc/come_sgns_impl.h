@@ -1,0 +1,805 @@
+// come_sgns_impl.h -- skip-gram negative-sampling updates for gfx950 (MI355X, CDNA4).
+//
+// Replaces the reference's Cython hot loop, /root/reference/utils/training_sdg_inner.pyx:
+//   fast0_o2/fast1_o2 (pyx:105-201) + train_o2 (pyx:454-509)   -> k_sgns_o2
+//   fast0_o1/fast1_o1 (pyx:205-296) + train_o1 (pyx:407-450)   -> k_sgns_o1
+//
+// Execution model:
+//  * One 64-lane wavefront owns one walk (O2) or one edge (O1) and processes its positive pairs in
+//    the reference's order, one pair at a time -- exactly the work one reference thread does per
+//    nogil call (pyx:493).  All walks/edges of a batch are in flight at once (Hogwild across
+//    wavefronts, as the reference's worker threads are Hogwild across walks).
+//  * A d-dim fp32 row is spread over the wave: lane l holds elements l, l+64, ... (VEC =
+//    ceil(d/64) of them); every row access is VEC wave instructions of 256 contiguous bytes.
+//  * The (1 + negative) target rows of a pair are gathered together, their dot products reduced
+//    with interleaved xor butterflies, then resolved in reference order (a negative that repeats an
+//    earlier target sees that target's updated row, pyx:147, via register forwarding).
+//  * Negatives never touch the host: lane k of the wave computes LCG draw (base + k) by jump-ahead
+//    (the LCG is affine mod 2^48, pyx:134) and gathers table[(s >> 16) % T] for 64 draws at once;
+//    each pair then reads its n draws with v_readlane (wave-uniform, scalar registers).
+//  * Dot product order is fixed: per-lane fmaf chain, then xor butterfly 1,2,4,8,16,32.  The CPU
+//    oracle's WAVE64 mode restates this order, so COME_MODE_SEQUENTIAL is bit-exact with it.
+//  * Compiled with -ffp-contract=off: every fused multiply-add is an explicit fmaf, matching the
+//    reference's saxpy (pyx:146-149) element for element.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "come_internal.h"
+
+namespace come {
+
+// One copy per translation unit (each .hip file is its own code object); come_init uploads the
+// table into every copy (upload_exp_table_vec*).
+static __constant__ float c_exp_table[kExpTableSize];
+
+struct LcgLane {  // this lane's jump-ahead (A^k, C_k): s_{b+k} = A^k s_b + C_k  (mod 2^48)
+    uint64_t a, c;
+};
+
+__device__ inline LcgLane lcg_lane_constants(int k) {
+    uint64_t a = 1, c = 0;
+    for (int i = 0; i < k; ++i) {
+        a = (a * kLcgMul) & kLcgMask;
+        c = (c * kLcgMul + kLcgAdd) & kLcgMask;
+    }
+    return {a, c};
+}
+
+__device__ inline uint64_t lcg_next(uint64_t s) { return (s * kLcgMul + kLcgAdd) & kLcgMask; }
+
+__device__ inline uint32_t table_slot(uint64_t s, uint64_t m, uint32_t d) {
+    const uint32_t x = (uint32_t)(s >> 16);  // < 2^32 because s < 2^48 (pyx:133)
+    if (d == 0) return x;                     // T >= 2^32: x % T == x
+    return (uint32_t)__umul64hi(m * (uint64_t)x, (uint64_t)d);
+}
+
+__device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline float uniformf(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ inline uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint32_t readlane_u32(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ inline uint64_t readlane_u64(uint64_t v, int lane) {
+    const uint32_t lo = readlane_u32((uint32_t)v, lane);
+    const uint32_t hi = readlane_u32((uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ---- row <-> registers -------------------------------------------------------------------------
+template <int VEC, bool FULL>
+struct Row {
+    float v[VEC];  // lane l holds elements l, l + 64, ..., l + 64 (VEC - 1)
+
+    // Every wave instruction touches 256 contiguous bytes (two 128-B lines): full-rate loads,
+    // stores and -- what fixes this layout -- full-rate float atomics (MI355X_MICROARCH.md
+    // "Global float atomics": 256 contiguous bytes per wave instruction).
+    __device__ inline void load(const float *__restrict__ row, int lane, int d) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const int e = lane + 64 * i;
+            v[i] = (FULL || e < d) ? row[e] : 0.0f;
+        }
+    }
+
+    __device__ inline void store(float *__restrict__ row, int lane, int d) const {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const int e = lane + 64 * i;
+            if (FULL || e < d) row[e] = v[i];
+        }
+    }
+
+    // row += v with no-return float atomics (Hogwild write-back: no update is lost)
+    __device__ inline void atomic_add(float *__restrict__ row, int lane, int d) const {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const int e = lane + 64 * i;
+            if (FULL || e < d) atomicAdd(row + e, v[i]);
+        }
+    }
+};
+
+template <int VEC, bool FULL>
+__device__ inline float lane_partial(const Row<VEC, FULL> &a, const Row<VEC, FULL> &b) {
+    float p = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) p = __builtin_fmaf(a.v[i], b.v[i], p);
+    return p;
+}
+
+// One stage of the 64-lane sum.  Stage s adds the partner group that differs in lane bit s, so
+// the tree is the xor butterfly over offsets 1, 2, 4, 8, 16, 32 (the oracle's WAVE64 order).
+// After each stage every lane of a group holds the same value (a + b == b + a bit for bit), so
+// any partner in the other group gives the same sum: DPP quad_perm for bits 0-1, row_half_mirror
+// / row_mirror for bits 2-3, and gfx950's v_permlane16_swap / v_permlane32_swap for bits 4-5
+// (all VALU: no LDS round trip, unlike ds_bpermute).
+template <int S>
+__device__ inline float reduce_stage(float p) {
+    const int x = __float_as_int(p);
+    if constexpr (S == 0) return p + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+    if constexpr (S == 1) return p + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+    if constexpr (S == 2) return p + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));
+    if constexpr (S == 3) return p + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));
+    if constexpr (S == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return __int_as_float(r[0]) + __int_as_float(r[1]);  // lower row + upper row, every lane
+    }
+    if constexpr (S == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return __int_as_float(r[0]) + __int_as_float(r[1]);  // lower half + upper half
+    }
+    return p;
+}
+
+__device__ inline float wave_sum(float p) {
+    p = reduce_stage<0>(p);
+    p = reduce_stage<1>(p);
+    p = reduce_stage<2>(p);
+    p = reduce_stage<3>(p);
+    p = reduce_stage<4>(p);
+    return reduce_stage<5>(p);
+}
+
+// Sum the first `count` of `part[]` across the wave, the six stages interleaved over the targets
+// so their latencies overlap.
+template <int N>
+__device__ inline void wave_sum_n(float (&part)[N], int count) {
+#define COME_STAGE(S)                                          \
+    _Pragma("unroll") for (int k = 0; k < N; ++k) if (k < count) part[k] = reduce_stage<S>(part[k]);
+    COME_STAGE(0) COME_STAGE(1) COME_STAGE(2) COME_STAGE(3) COME_STAGE(4) COME_STAGE(5)
+#undef COME_STAGE
+}
+
+// sigma lookup exactly as generated from pyx:141-143: skip if f <= -6 or f >= 6, else
+// EXP_TABLE[(int)(((double)f + 6.0) * 83.0)].  Returns false for a skipped target.
+__device__ inline bool sigmoid_ref(float f, float *sig) {
+    if (f <= -(float)kMaxExp || f >= (float)kMaxExp) return false;
+    const int b = (int)(((double)f + 6.0) * 83.0);
+    *sig = c_exp_table[b];
+    return true;
+}
+
+// ---- batch of 64 negative draws held one per lane ------------------------------------------
+struct DrawBatch {
+    uint32_t target;  // this lane's table value for draw (base + lane)
+    uint64_t base;    // LCG state of draw `base`'s index 0 (wave-uniform)
+    int used;         // draws of the batch already consumed (wave-uniform)
+};
+
+__device__ inline void draws_fill(DrawBatch &b, uint64_t state0, const LcgLane &lc,
+                                  const uint32_t *__restrict__ table, FastMod fm, int64_t V) {
+    b.base = state0;
+    b.used = 0;
+    const uint64_t s = (lc.a * state0 + lc.c) & kLcgMask;
+    const uint32_t slot = table_slot(s, fm.m, fm.d);
+    uint32_t t = table[slot];
+    b.target = t;
+}
+
+// State of the draw `b.used` positions after the batch base (0 < used <= 64).
+__device__ inline uint64_t draws_state_at_used(const DrawBatch &b, const LcgLane &lc) {
+    const uint64_t s = (lc.a * b.base + lc.c) & kLcgMask;  // this lane's state
+    if (b.used < 64) return uniform64(readlane_u64(s, b.used));
+    return lcg_next(uniform64(readlane_u64(s, 63)));
+}
+
+// Double-buffered draws: lanes of t0 hold draws base0 + lane, lanes of t1 the next 64.  The next
+// batch's table gather is issued as soon as the current one starts, so a pair never waits for
+// the table.  take(k) = target of draw `used + k` (used + k < 128).
+struct DrawPipe {
+    uint32_t t0, t1;
+    uint64_t base0, base1;
+    int used;
+
+    template <class Args>
+    __device__ inline uint32_t gather(uint64_t base, const LcgLane &lc, const Args &a) {
+        const uint64_t s = (lc.a * base + lc.c) & kLcgMask;  // draw base + lane
+        return a.table[table_slot(s, a.fm.m, a.fm.d)];
+    }
+};
+
+// ---- O2: one wavefront per walk ------------------------------------------------------------
+
+struct O2Args {
+    float *node;
+    float *ctx;
+    const int32_t *walks;
+    const uint64_t *seeds;
+    const uint32_t *table;
+    int64_t V;
+    int64_t P;
+    int L;
+    int d;
+    int window;
+    int negative;
+    float lr;
+    float alpha;
+    FastMod fm;
+};
+
+// State 64 draws after `base` (lane 63's state advanced once).
+__device__ inline uint64_t advance64(uint64_t base, const LcgLane &lc) {
+    const uint64_t s = (lc.a * base + lc.c) & kLcgMask;
+    return lcg_next(uniform64(readlane_u64(s, 63)));
+}
+
+// One O2 pair (pyx:105-151) with the input row `in` and the positive row `pos` already in
+// registers.  Draws the pair's n negatives (pyx:133-135), gathers their rows, reduces every dot
+// product, resolves the targets in reference order, stores the updated negative rows, updates
+// `pos` in registers (pos_upd |= updated) and finally applies `in += work` (pyx:149).
+template <int VEC, bool FULL, int MAXN>
+__device__ inline void o2_pair(const O2Args &a, DrawBatch &db, const LcgLane &lc, int lane, int ci,
+                               Row<VEC, FULL> &pos, bool &pos_upd, Row<VEC, FULL> &in,
+                               Row<VEC, FULL> &work) {
+    using R = Row<VEC, FULL>;
+    const int n = a.negative;
+    const int d = a.d;
+    if (n > 0 && db.used + n > 64) draws_fill(db, draws_state_at_used(db, lc), lc, a.table, a.fm, a.V);
+    int t[MAXN + 1];
+    bool valid[MAXN + 1];
+    t[0] = ci;
+    valid[0] = true;
+#pragma unroll
+    for (int k = 1; k <= MAXN; ++k) {
+        if (k <= n) {
+            const int tk = (int)readlane_u32(db.target, db.used + k - 1);
+            t[k] = tk;
+            // pyx:135 skip == positive; out-of-range table values skipped (no OOB)
+            valid[k] = tk != ci && tk >= 0 && tk < a.V;
+        } else {
+            t[k] = -1;
+            valid[k] = false;
+        }
+    }
+    if (n > 0) db.used += n;
+
+    R r[MAXN + 1];
+#pragma unroll
+    for (int k = 1; k <= MAXN; ++k)
+        if (valid[k]) r[k].load(a.ctx + (int64_t)t[k] * d, lane, d);
+
+    // dots of every target against the (fixed) input row, butterflies interleaved
+    float part[MAXN + 1];
+    part[0] = lane_partial(in, pos);
+#pragma unroll
+    for (int k = 1; k <= MAXN; ++k) part[k] = valid[k] ? lane_partial(in, r[k]) : 0.0f;
+    wave_sum_n(part, n + 1);
+
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) work.v[e] = 0.0f;
+    // positive (d == 0, label 1)
+    {
+        float sig;
+        if (sigmoid_ref(uniformf(part[0]), &sig)) {
+            const float g = ((1.0f - sig) * a.lr) * a.alpha;  // pyx:144
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                work.v[e] = __builtin_fmaf(g, pos.v[e], work.v[e]);  // pyx:146
+                pos.v[e] = __builtin_fmaf(g, in.v[e], pos.v[e]);     // pyx:147
+            }
+            pos_upd = true;
+        }
+    }
+    bool upd[MAXN + 1];
+    upd[0] = false;
+#pragma unroll
+    for (int k = 1; k <= MAXN; ++k) {
+        upd[k] = false;
+        if (!valid[k]) continue;
+        float f = part[k];
+        // A repeated negative sees the row as left by its latest earlier occurrence.
+        int prev = -1;
+#pragma unroll
+        for (int q = 1; q < k; ++q)
+            if (valid[q] && t[q] == t[k]) prev = q;
+        if (prev >= 0) {
+#pragma unroll
+            for (int q = 1; q < k; ++q) {
+                if (q == prev) {
+                    r[k] = r[q];
+                    f = upd[q] ? wave_sum(lane_partial(in, r[k])) : part[q];
+                }
+            }
+        }
+        f = uniformf(f);
+        part[k] = f;  // effective dot of this occurrence (a later repeat may reuse it)
+        float sig;
+        if (!sigmoid_ref(f, &sig)) continue;  // pyx:141-142
+        const float g = ((0.0f - sig) * a.lr) * a.alpha;  // pyx:144, label 0
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            work.v[e] = __builtin_fmaf(g, r[k].v[e], work.v[e]);  // pyx:146
+            r[k].v[e] = __builtin_fmaf(g, in.v[e], r[k].v[e]);    // pyx:147
+        }
+        upd[k] = true;
+    }
+    // write back in order, so a repeated row ends with its last version
+#pragma unroll
+    for (int k = 1; k <= MAXN; ++k)
+        if (upd[k]) r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) in.v[e] = in.v[e] + work.v[e];  // pyx:149
+}
+
+template <int VEC, bool FULL>
+__device__ inline void atomic_add_delta(float *__restrict__ row, const Row<VEC, FULL> &cur,
+                                        const Row<VEC, FULL> &orig, int lane, int d) {
+    Row<VEC, FULL> delta;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) delta.v[e] = cur.v[e] - orig.v[e];
+    delta.atomic_add(row, lane, d);
+}
+
+// Direct variant: every pair reads and writes its input and positive rows in HBM.  Used when the
+// LDS ring of the cached variant would not fit (large window x d).
+template <int VEC, bool FULL, int MAXN>
+__global__ void __launch_bounds__(256) k_sgns_o2(O2Args a) {
+    using R = Row<VEC, FULL>;
+    const int lane = threadIdx.x & 63;
+    const int64_t waves_per_block = blockDim.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * waves_per_block;
+    const LcgLane lc = lcg_lane_constants(lane);
+    const int d = a.d;
+    const int path_len = a.L < kMaxSentenceLen ? a.L : kMaxSentenceLen;  // pyx:480
+
+    for (int64_t p = gw; p < a.P; p += nwaves) {
+        const int32_t *__restrict__ idx = a.walks + p * (int64_t)a.L;
+        DrawBatch db;
+        db.used = 0;
+        db.base = uniform64(a.seeds[p]);
+        db.target = 0;
+        if (a.negative > 0) draws_fill(db, db.base, lc, a.table, a.fm, a.V);
+        for (int i = 0; i < path_len; ++i) {
+            const int ci = uniform(idx[i]);
+            if (ci < 0 || ci >= a.V) continue;  // codelens[i] == 0 (pyx:495)
+            const int j0 = i - a.window < 0 ? 0 : i - a.window;
+            const int j1 = i + a.window + 1 > path_len ? path_len : i + a.window + 1;
+            for (int j = j0; j < j1; ++j) {
+                if (j == i) continue;
+                const int cj = uniform(idx[j]);
+                if (cj < 0 || cj >= a.V) continue;  // pyx:504
+                R in, pos;
+                in.load(a.node + (int64_t)cj * d, lane, d);
+                pos.load(a.ctx + (int64_t)ci * d, lane, d);
+                bool pos_upd = false;
+                R work;
+                o2_pair<VEC, FULL, MAXN>(a, db, lc, lane, ci, pos, pos_upd, in, work);
+                if (pos_upd) pos.store(a.ctx + (int64_t)ci * d, lane, d);
+                in.store(a.node + (int64_t)cj * d, lane, d);
+            }
+        }
+    }
+}
+
+// Cached, software-pipelined variant (the hot kernel).
+//
+// Traffic cuts, exact in sequential order:
+//  * the center's positive row ctx[idx[i]] stays in registers across its 2w pairs (no negative of
+//    those pairs can be that row: pyx:135 skips it) and is written back once per center;
+//  * the input rows of the window [i-w, i+w] live in a per-wavefront LDS ring of 2w+1 rows: a
+//    walk position's node row is read from HBM once, when it enters the window, instead of once
+//    per pair.  Positions holding the same node id alias: entering copies the live LDS row, every
+//    update is applied to all aliases.
+// Latency hiding (one wavefront walks its pairs strictly in order, so memory-level parallelism
+// has to come from running ahead):
+//  * the walk's row indices sit in two VGPR chunks of 64 positions (v_readlane), refilled 64
+//    positions ahead -- no dependent index loads;
+//  * the next pair's negative rows are loaded while the current pair computes, the next center's
+//    positive row and entering node row while the current center runs, the next 64 table draws
+//    while the current 64 are consumed.  Every prefetched row that the current work writes before
+//    it is used is replaced by the register copy (forwarding), so sequential order is preserved
+//    bit for bit.  Prefetch loads are unconditional (out-of-range targets read row 0 and are
+//    discarded) so the compiler's vmcnt waits stay counted, never vmcnt(0).
+// Write-back.  SEQ (one wavefront, the parity mode): plain stores -- the positive once per center,
+// a node row when its last alias leaves the window.  HOG (all walks in flight): every pair adds
+// its `work` to the node row with float atomics and every center adds its positive row's change
+// (cur - orig), so a row several wavefronts hold at once (a hub) loses none of their updates; the
+// LDS / register copies are the wavefront's own Hogwild view.  Negative rows are read-modify-
+// written per pair with plain loads and stores in both modes, as the reference's saxpy does.
+template <int VEC, bool FULL, int MAXN, bool HOG>
+__global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
+    using R = Row<VEC, FULL>;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const int64_t waves_per_block = blockDim.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * waves_per_block + wib;
+    const int64_t nwaves = (int64_t)gridDim.x * waves_per_block;
+    const LcgLane lc = lcg_lane_constants(lane);
+    const int d = a.d;
+    const int w = a.window;
+    const int n = a.negative;
+    const int RS = 2 * w + 1;  // ring slots (<= 64: ids live one per lane)
+    const int path_len = a.L < kMaxSentenceLen ? a.L : kMaxSentenceLen;  // pyx:480
+    const int wave_floats = (RS * d + 3) & ~3;
+    float *ring = lds + wib * wave_floats;
+    auto valid_row = [&](int r) { return r >= 0 && r < a.V; };
+    auto slot_add = [&](int s, int delta) {  // (s + delta) mod RS for |delta| <= RS
+        s += delta;
+        if (s < 0) s += RS;
+        if (s >= RS) s -= RS;
+        return s;
+    };
+
+    for (int64_t p = gw; p < a.P; p += nwaves) {
+        const int32_t *__restrict__ walk = a.walks + p * (int64_t)a.L;
+        // ---- walk indices: positions [wbase, wbase + 128) in two VGPR chunks ----
+        int wbase = 0;
+        int c0 = lane < path_len ? walk[lane] : -1;
+        int c1 = 64 + lane < path_len ? walk[64 + lane] : -1;
+        auto idx_at = [&](int q) {  // validated row of walk position q (-1 = None / past the end)
+            if (q >= path_len) return -1;
+            const int off = q - wbase;
+            const int r = off < 64 ? __builtin_amdgcn_readlane(c0, off)
+                                   : __builtin_amdgcn_readlane(c1, off - 64);
+            return valid_row(r) ? r : -1;
+        };
+        // ---- draws ----
+        DrawPipe dp;
+        dp.used = 0;
+        dp.base0 = uniform64(a.seeds[p]);
+        dp.t0 = dp.t1 = 0;
+        if (n > 0) {
+            dp.t0 = dp.gather(dp.base0, lc, a);
+            dp.base1 = advance64(dp.base0, lc);
+            dp.t1 = dp.gather(dp.base1, lc, a);
+        }
+        auto take = [&](int k) -> int {
+            const int q = dp.used + k;
+            return (int)(q < 64 ? readlane_u32(dp.t0, q) : readlane_u32(dp.t1, q - 64));
+        };
+        auto advance = [&]() {
+            if (n == 0) return;
+            dp.used += n;
+            if (dp.used >= 64) {
+                dp.used -= 64;
+                dp.t0 = dp.t1;
+                dp.base0 = dp.base1;
+                dp.base1 = advance64(dp.base1, lc);
+                dp.t1 = dp.gather(dp.base1, lc, a);
+            }
+        };
+        // next pair's negatives: raw targets and their rows (row 0 stands in for bad targets)
+        int tn[MAXN + 1];
+        R rn[MAXN + 1];
+        auto fetch_next = [&]() {
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                const int tk = k <= n ? take(k - 1) : -1;
+                tn[k] = tk;
+                rn[k].load(a.ctx + (int64_t)(valid_row(tk) ? tk : 0) * d, lane, d);
+            }
+        };
+        fetch_next();
+
+        // ---- ring (LDS rows) + ids (one per lane) ----
+        int ids = -1;  // lane s: node row held by ring slot s
+        auto id_of = [&](int s) { return __builtin_amdgcn_readlane(ids, s); };
+        auto alias_mask = [&](int id, int except) -> uint64_t {
+            return __ballot(lane < RS && lane != except && ids == id);
+        };
+        auto set_id = [&](int s, int id) { ids = lane == s ? id : ids; };
+        auto write_back = [&](int s, int id) {  // SEQ: last holder stores the row
+            if (!HOG && alias_mask(id, s) == 0) {
+                R row;
+                row.load(ring + s * d, lane, d);
+                row.store(a.node + (int64_t)id * d, lane, d);
+            }
+        };
+        auto enter_row = [&](int s, int id, const R &fetched) {  // fetched: node[id] loaded earlier
+            const uint64_t m = alias_mask(id, s);
+            if (m) {
+                R row;
+                row.load(ring + __builtin_ctzll(m) * d, lane, d);
+                row.store(ring + s * d, lane, d);
+            } else {
+                fetched.store(ring + s * d, lane, d);
+            }
+            set_id(s, id);
+        };
+        for (int q = 0; q < w && q < path_len; ++q) {  // positions [0, w) before center 0
+            const int id = idx_at(q);
+            if (id >= 0) {
+                R row;
+                row.load(a.node + (int64_t)id * d, lane, d);
+                enter_row(q, id, row);
+            }
+        }
+        // center-level prefetch: the positive of the next center, the row entering with it
+        R pos_n, ent_n;
+        int pos_n_id = idx_at(0), ent_n_id = idx_at(w);
+        pos_n.load(a.ctx + (int64_t)(pos_n_id >= 0 ? pos_n_id : 0) * d, lane, d);
+        ent_n.load(a.node + (int64_t)(ent_n_id >= 0 ? ent_n_id : 0) * d, lane, d);
+
+        int si = 0;  // slot of position i
+        for (int i = 0; i < path_len; ++i) {
+            // this center's prefetched rows, then prefetch for center i+1
+            if (i + 1 + w >= wbase + 128) {  // keep [i, i + 1 + w] inside the two chunks
+                wbase += 64;
+                c0 = c1;
+                c1 = wbase + 64 + lane < path_len ? walk[wbase + 64 + lane] : -1;
+            }
+            const int ci = pos_n_id;
+            R pos = pos_n;
+            // ring: position i-w-1 leaves, position i+w enters (same slot)
+            const int se = slot_add(si, w);
+            if (i + w < path_len || i - w - 1 >= 0) {
+                const int old_id = i - w - 1 >= 0 ? id_of(se) : -1;
+                if (old_id >= 0 && old_id == ent_n_id) {
+                    // the same node leaves and enters: keep the live LDS row (no store, no load)
+                } else {
+                    if (old_id >= 0) write_back(se, old_id);
+                    set_id(se, -1);
+                    if (i + w < path_len && ent_n_id >= 0) enter_row(se, ent_n_id, ent_n);
+                }
+            }
+            // prefetch for center i+1, after this boundary's write-back (a node that just left
+            // may be the one entering next; its prefetched copy must not predate the store)
+            pos_n_id = idx_at(i + 1);
+            ent_n_id = idx_at(i + 1 + w);
+            pos_n.load(a.ctx + (int64_t)(pos_n_id >= 0 ? pos_n_id : 0) * d, lane, d);
+            ent_n.load(a.node + (int64_t)(ent_n_id >= 0 ? ent_n_id : 0) * d, lane, d);
+
+            if (ci >= 0) {  // codelens[i] != 0 (pyx:495)
+                R pos0;
+                if (HOG) pos0 = pos;
+                bool pos_upd = false;
+                const int j0 = i - w < 0 ? 0 : i - w;
+                const int j1 = i + w + 1 > path_len ? path_len : i + w + 1;
+                for (int j = j0; j < j1; ++j) {
+                    if (j == i) continue;
+                    const int sj = slot_add(si, j - i);
+                    const int cj = id_of(sj);
+                    if (cj < 0) continue;  // pyx:504
+                    R in;
+                    in.load(ring + sj * d, lane, d);
+                    // this pair's negatives were prefetched; put the next pair's in flight
+                    int t[MAXN + 1];
+                    R r[MAXN + 1];
+#pragma unroll
+                    for (int k = 1; k <= MAXN; ++k) {
+                        t[k] = tn[k];
+                        r[k] = rn[k];
+                    }
+                    advance();
+                    fetch_next();
+
+                    // ---- the pair (pyx:128-149) ----
+                    bool valid[MAXN + 1];
+#pragma unroll
+                    for (int k = 1; k <= MAXN; ++k)
+                        valid[k] = k <= n && t[k] != ci && valid_row(t[k]);  // pyx:135
+                    float part[MAXN + 1];
+                    part[0] = lane_partial(in, pos);
+#pragma unroll
+                    for (int k = 1; k <= MAXN; ++k) part[k] = lane_partial(in, r[k]);
+                    wave_sum_n(part, n + 1);
+                    R work;
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) work.v[e] = 0.0f;
+                    {
+                        float sig;
+                        if (sigmoid_ref(uniformf(part[0]), &sig)) {
+                            const float g = ((1.0f - sig) * a.lr) * a.alpha;  // pyx:144
+#pragma unroll
+                            for (int e = 0; e < VEC; ++e) {
+                                work.v[e] = __builtin_fmaf(g, pos.v[e], work.v[e]);  // pyx:146
+                                pos.v[e] = __builtin_fmaf(g, in.v[e], pos.v[e]);     // pyx:147
+                            }
+                            pos_upd = true;
+                        }
+                    }
+                    bool upd[MAXN + 1];
+#pragma unroll
+                    for (int k = 1; k <= MAXN; ++k) {
+                        upd[k] = false;
+                        if (!valid[k]) continue;
+                        float f = part[k];
+                        int prev = -1;  // latest earlier occurrence of the same negative row
+#pragma unroll
+                        for (int q = 1; q < k; ++q)
+                            if (valid[q] && t[q] == t[k]) prev = q;
+                        if (prev >= 0) {
+#pragma unroll
+                            for (int q = 1; q < k; ++q) {
+                                if (q == prev) {
+                                    r[k] = r[q];
+                                    f = upd[q] ? wave_sum(lane_partial(in, r[k])) : part[q];
+                                }
+                            }
+                        }
+                        f = uniformf(f);
+                        part[k] = f;
+                        float sig;
+                        if (!sigmoid_ref(f, &sig)) continue;  // pyx:141-142
+                        const float g = ((0.0f - sig) * a.lr) * a.alpha;  // pyx:144, label 0
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) {
+                            work.v[e] = __builtin_fmaf(g, r[k].v[e], work.v[e]);  // pyx:146
+                            r[k].v[e] = __builtin_fmaf(g, in.v[e], r[k].v[e]);    // pyx:147
+                        }
+                        upd[k] = true;
+                    }
+#pragma unroll
+                    for (int k = 1; k <= MAXN; ++k) {
+                        if (!upd[k]) continue;
+                        r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+                        // prefetched copies of this row are now stale: forward the new value
+#pragma unroll
+                        for (int q = 1; q <= MAXN; ++q)
+                            if (tn[q] == t[k]) rn[q] = r[k];
+                        if (pos_n_id == t[k]) pos_n = r[k];
+                    }
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) in.v[e] = in.v[e] + work.v[e];  // pyx:149
+                    if (HOG) work.atomic_add(a.node + (int64_t)cj * d, lane, d);
+                    uint64_t m = alias_mask(cj, -1);  // the slot and every alias of it
+                    while (m) {
+                        const int rr = __builtin_ctzll(m);
+                        m &= m - 1;
+                        in.store(ring + rr * d, lane, d);
+                    }
+                }
+                if (pos_upd) {
+                    if (HOG) atomic_add_delta(a.ctx + (int64_t)ci * d, pos, pos0, lane, d);
+                    else pos.store(a.ctx + (int64_t)ci * d, lane, d);
+#pragma unroll
+                    for (int q = 1; q <= MAXN; ++q)
+                        if (tn[q] == ci) rn[q] = pos;  // prefetched before this write-back
+                    if (pos_n_id == ci) pos_n = pos;
+                }
+            }
+            si = slot_add(si, 1);
+        }
+        // positions still in the ring leave in order
+        const int first = path_len - w - 1 > 0 ? path_len - w - 1 : 0;
+        for (int q = first; q < path_len; ++q) {
+            const int s = q % RS;
+            const int id = id_of(s);
+            if (id >= 0) write_back(s, id);
+            set_id(s, -1);
+        }
+    }
+}
+
+// ---- O1: one wavefront per edge ------------------------------------------------------------
+struct O1Args {
+    float *node;
+    const int32_t *edges;
+    const uint64_t *seeds;
+    const uint32_t *table;
+    int64_t V;
+    int64_t E;
+    int d;
+    int negative;
+    float lr;
+    FastMod fm;
+};
+
+template <int VEC, bool FULL, int MAXN>
+__global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
+    using R = Row<VEC, FULL>;
+    const int lane = threadIdx.x & 63;
+    const int64_t waves_per_block = blockDim.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * waves_per_block;
+    const LcgLane lc = lcg_lane_constants(lane);
+    const int n = a.negative;
+    const int d = a.d;
+
+    for (int64_t e = gw; e < a.E; e += nwaves) {
+        const int u = uniform(a.edges[2 * e]);
+        const int v = uniform(a.edges[2 * e + 1]);
+        if (u < 0 || u >= a.V || v < 0 || v >= a.V) continue;  // reference: undefined behaviour
+        // 2n draws: pair 1 uses draws 0..n-1, pair 2 draws n..2n-1 (state carried, pyx:444-448)
+        DrawBatch db;
+        db.used = 0;
+        db.base = uniform64(a.seeds[e]);
+        db.target = 0;
+        if (n > 0) draws_fill(db, db.base, lc, a.table, a.fm, a.V);
+
+        int t1[MAXN + 1], t2[MAXN + 1];
+        bool v1[MAXN + 1], v2[MAXN + 1];
+        t1[0] = v;  // pair 1: input u, positive v (pyx:444)
+        t2[0] = u;  // pair 2: input v, positive u (pyx:447)
+        v1[0] = v2[0] = true;
+#pragma unroll
+        for (int k = 1; k <= MAXN; ++k) {
+            if (k <= n) {
+                t1[k] = (int)readlane_u32(db.target, k - 1);
+                t2[k] = (int)readlane_u32(db.target, n + k - 1);
+                v1[k] = t1[k] != v && t1[k] >= 0 && t1[k] < a.V;
+                v2[k] = t2[k] != u && t2[k] >= 0 && t2[k] < a.V;
+            } else {
+                t1[k] = t2[k] = -1;
+                v1[k] = v2[k] = false;
+            }
+        }
+        // Every row both pairs read can be gathered up front: pair 1 writes only node[u]; pair 2
+        // never reads node[u] through a negative (skipped, == its positive) and gets its positive
+        // (and, for a self-loop, its input) forwarded from pair 1's registers.
+        R in1, in2;
+        in1.load(a.node + (int64_t)u * d, lane, d);
+        if (v != u) in2.load(a.node + (int64_t)v * d, lane, d);
+        R r1[MAXN + 1], r2[MAXN + 1];
+#pragma unroll
+        for (int k = 1; k <= MAXN; ++k) {
+            if (v1[k]) r1[k].load(a.node + (int64_t)t1[k] * d, lane, d);
+            if (v2[k]) r2[k].load(a.node + (int64_t)t2[k] * d, lane, d);
+        }
+        if (v != u) r1[0] = in2; else r1[0] = in1;  // positive of pair 1 = node[v] (pre-update)
+
+        // pair 1
+        {
+            float part[MAXN + 1];
+#pragma unroll
+            for (int k = 0; k <= MAXN; ++k) part[k] = v1[k] ? lane_partial(in1, r1[k]) : 0.0f;
+            wave_sum_n(part, n + 1);
+            R work;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) work.v[q] = 0.0f;
+#pragma unroll
+            for (int k = 0; k <= MAXN; ++k) {
+                if (!v1[k]) continue;
+                float sig;
+                if (!sigmoid_ref(uniformf(part[k]), &sig)) continue;
+                const float g = ((k == 0 ? 1.0f : 0.0f) - sig) * a.lr;  // pyx:243
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) work.v[q] = __builtin_fmaf(g, r1[k].v[q], work.v[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) in1.v[q] = in1.v[q] + work.v[q];  // pyx:247
+            in1.store(a.node + (int64_t)u * d, lane, d);
+        }
+        // pair 2: positive = node[u] as pair 1 left it; self-loop: the input is that row too.
+        r2[0] = in1;
+        if (v == u) in2 = in1;
+        {
+            float part[MAXN + 1];
+#pragma unroll
+            for (int k = 0; k <= MAXN; ++k) part[k] = v2[k] ? lane_partial(in2, r2[k]) : 0.0f;
+            wave_sum_n(part, n + 1);
+            R work;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) work.v[q] = 0.0f;
+#pragma unroll
+            for (int k = 0; k <= MAXN; ++k) {
+                if (!v2[k]) continue;
+                float sig;
+                if (!sigmoid_ref(uniformf(part[k]), &sig)) continue;
+                const float g = ((k == 0 ? 1.0f : 0.0f) - sig) * a.lr;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) work.v[q] = __builtin_fmaf(g, r2[k].v[q], work.v[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) in2.v[q] = in2.v[q] + work.v[q];
+            in2.store(a.node + (int64_t)v * d, lane, d);
+        }
+    }
+}
+
+// Kernel entry addresses per instantiation (defined in come_sgns_vec{1,2,4,8}.hip so the
+// instantiations compile in parallel).
+struct KernelSet {
+    void *o2_direct[2][3];   // [FULL][maxn idx]
+    void *o2_ring[2][3][2];  // [FULL][maxn idx][HOG]
+    void *o1[2][3];
+};
+#define COME_DECLARE_VEC(V) \
+    const KernelSet &kernels_vec##V(); \
+    hipError_t upload_exp_table_vec##V(const float *host1000);
+COME_DECLARE_VEC(1)
+COME_DECLARE_VEC(2)
+COME_DECLARE_VEC(4)
+COME_DECLARE_VEC(8)
+#undef COME_DECLARE_VEC
+
+}  // namespace come

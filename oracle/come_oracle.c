@@ -17,8 +17,8 @@
  *                        Differs from OpenBLAS' own summation order by ~1 ulp, which is why the
  *                        reference comparison is tolerance-based (SURVEY.md §8c tiers A/B).
  *   COME_DOT_WAVE64 (1): the exact summation tree of the HIP kernel (lane l holds elements
- *                        l*VEC .. l*VEC+VEC-1 accumulated by an fmaf chain, then an xor butterfly
- *                        over offsets 32,16,8,4,2,1).  With this order the GPU sequential mode must
+ *                        l, l+64, ..., accumulated by an fmaf chain in that order, then an xor
+ *                        butterfly over offsets 1,2,4,8,16,32).  With this order the GPU sequential mode must
  *                        agree with this oracle BIT FOR BIT.
  * Build: see oracle/Makefile (-O2 -ffp-contract=off, no fast-math: every fmaf below is explicit).
  */
@@ -80,12 +80,12 @@ static float dot_wave64(const float *a, const float *b, int d) {
     for (int l = 0; l < 64; ++l) {
         float p = 0.0f;
         for (int v = 0; v < vec; ++v) {
-            int e = l * vec + v;
+            int e = l + 64 * v;
             if (e < d) p = fmaf(a[e], b[e], p);
         }
         lane[l] = p;
     }
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = 1; off <= 32; off <<= 1) {
         float t[64];
         for (int l = 0; l < 64; ++l) t[l] = lane[l] + lane[l ^ off];
         memcpy(lane, t, sizeof(t));

@@ -11,8 +11,8 @@ BENCH="$ROOT/bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline ${BENCH_A
 fatal() { [ "$1" -ne 0 ] && { echo "fatal rc=$1 in $2"; exit "$1"; }; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err"
 fatal $? trace
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o run -- python3 $BENCH > "$OUT/pmc_${C}_bench.json" 2> "$OUT/pmc_${C}_bench.err"
+for C in FETCH_SIZE WRITE_SIZE ${EXTRA_PMC}; do
+  timeout -k 10 400 rocprofv3 --pmc ${C//,/ } --output-format csv -d "$OUT/pmc_$C" -o run -- python3 $BENCH > "$OUT/pmc_${C}_bench.json" 2> "$OUT/pmc_${C}_bench.err"
   fatal $? pmc_$C
 done
 find "$OUT" -name "*.csv" | head -20

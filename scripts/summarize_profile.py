@@ -13,7 +13,7 @@ import os
 import shutil
 import sys
 
-KERNEL = "k_sgns_o2"
+KERNEL = "k_sgns_o2"  # matches k_sgns_o2 and k_sgns_o2_ring
 
 
 def main(src, tag, kernel=KERNEL):
