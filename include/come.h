@@ -98,6 +98,12 @@ int come_community_grad(float *x, int64_t V, int d, const float *pi, const float
 int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
                   const float *log_norm, int K, float *resp_out, void *stream);
 
+/* ---- Tuning ----
+ * Process-wide launch knobs for experiments (0 = automatic): "o2_kernel" (1 direct, 2 ring),
+ * "o2_blocks_per_cu", "o2_waves_per_block", "o2_plain_writeback" (1 = Hogwild with plain-store
+ * write-back of cached rows: faster but loses concurrent updates; not the default). */
+int come_set_option(const char *name, int value);
+
 /* ---- Host helpers ---- */
 
 /* Model.make_table (model.py:97-122), exact: same double accumulation, same start at node id 1,

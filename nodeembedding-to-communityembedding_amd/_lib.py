@@ -15,7 +15,7 @@ MODE_SEQUENTIAL = 1
 # Every symbol include/come.h declares (checked by tests/test_capi.py).
 SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_fast_version", "come_sgns_o2", "come_sgns_o1", "come_community_grad",
-           "come_gmm_resp", "come_make_table", "come_count_o2_pairs")
+           "come_gmm_resp", "come_make_table", "come_count_o2_pairs", "come_set_option")
 
 _lib = None
 
@@ -53,6 +53,7 @@ def lib():
     L.come_make_table.argtypes = [P, i64, P, u64, f64]
     L.come_count_o2_pairs.argtypes = [P, i64, i32, i32]
     L.come_count_o2_pairs.restype = i64
+    L.come_set_option.argtypes = [ctypes.c_char_p, i32]
     if L.come_abi_version() != 1:
         raise ComeError("libcome.so ABI version mismatch")
     _lib = L
@@ -75,3 +76,8 @@ def ptr(t):
 def stream_handle(device=None):
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def set_option(name, value):
+    """Launch tuning knob (see include/come.h come_set_option)."""
+    check(lib().come_set_option(name.encode(), int(value)), "come_set_option(%s)" % name)

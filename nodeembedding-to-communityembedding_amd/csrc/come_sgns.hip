@@ -1,10 +1,18 @@
 // come_sgns.hip -- launchers and C-ABI entry points of the SGNS kernels (come_sgns_impl.h).
+#include <string.h>
+
 #include "come_sgns_impl.h"
 
 namespace come {
 
 constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr size_t kRingMaxWaveBytes = 40 * 1024;
+
+// Tuning / experiment knobs (come_set_option); 0 = automatic.
+static int g_opt_o2_kernel = 0;         // 1 = direct kernel, 2 = ring kernel
+static int g_opt_o2_blocks_per_cu = 0;  // grid cap override
+static int g_opt_o2_plain_writeback = 0;  // 1 = Hogwild with plain-store write-back (lossy)
+static int g_opt_o2_waves_per_block = 0;
 
 // ---- launchers -----------------------------------------------------------------------------
 static const KernelSet &kernel_set(int d, int *full) {
@@ -92,14 +100,21 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
     // LDS ring of the cached kernel: (2w+1) rows + their ids, per wave
     const int rs = 2 * window + 1;
     const size_t wave_bytes = 4 * (size_t)((rs * d + 3) & ~3);
-    if (rs <= 64 && wave_bytes <= kRingMaxWaveBytes) {
-        const int wpb = 2;
+    const bool ring_ok = rs <= 64 && wave_bytes <= kRingMaxWaveBytes;
+    if (g_opt_o2_kernel != 1 && ring_ok) {
+        // __launch_bounds__(128): at most 2 wavefronts per workgroup
+        const int wpb = g_opt_o2_waves_per_block == 1 ? 1 : 2;
         const size_t lds = wave_bytes * (hog ? wpb : 1);
-        const int per_cu = (int)(kLdsPerCu / (wave_bytes * wpb));
-        return launch(ks.o2_ring[full][mi][hog ? 1 : 0], &a, P, mode, wpb,
-                      per_cu < 1 ? 1 : (per_cu > 16 ? 16 : per_cu), lds, stream);
+        // 24 wavefronts per CU measured best on MI355X (d=128, n=5: 16/20/24/28 waves ->
+        // 141/123/110/132 ms per 1e8-pair launch, scripts/ab_o2.py): more in flight thrashes.
+        int per_cu = (int)(kLdsPerCu / (wave_bytes * wpb));
+        per_cu = per_cu < 1 ? 1 : (per_cu > 24 / wpb ? 24 / wpb : per_cu);
+        if (g_opt_o2_blocks_per_cu > 0) per_cu = g_opt_o2_blocks_per_cu;
+        const int variant = (hog && !g_opt_o2_plain_writeback) ? 1 : 0;
+        return launch(ks.o2_ring[full][mi][variant], &a, P, mode, wpb, per_cu, lds, stream);
     }
-    return launch(ks.o2_direct[full][mi], &a, P, mode, 4, 8, 0, stream);
+    return launch(ks.o2_direct[full][mi], &a, P, mode, 4,
+                  g_opt_o2_blocks_per_cu > 0 ? g_opt_o2_blocks_per_cu : 6, 0, stream);
 }
 
 extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
@@ -128,4 +143,21 @@ extern "C" int come_upload_exp_table(const float *host1000) {
         if (rc) return rc;
     }
     return COME_OK;
+}
+
+extern "C" int come_set_option(const char *name, int value) {
+    if (!name) return set_error(COME_E_INVALID, "null option name");
+    struct {
+        const char *k;
+        int *v;
+    } opts[] = {{"o2_kernel", &g_opt_o2_kernel},
+                {"o2_blocks_per_cu", &g_opt_o2_blocks_per_cu},
+                {"o2_plain_writeback", &g_opt_o2_plain_writeback},
+                {"o2_waves_per_block", &g_opt_o2_waves_per_block}};
+    for (auto &o : opts)
+        if (!strcmp(o.k, name)) {
+            *o.v = value;
+            return COME_OK;
+        }
+    return set_error(COME_E_INVALID, "unknown option '%s'", name);
 }

@@ -83,6 +83,8 @@ def test_o2_kat_bit_exact_vs_oracle_and_golden(name):
     (128, 10, 5, 40, 30, 8, 3000),       # small V: many repeated negatives / positive hits
     (256, 10, 5, 500, 40, 6, 20000),
     (512, 3, 2, 300, 20, 4, 5000),
+    (512, 3, 10, 300, 30, 3, 5000),      # ring would exceed 40 KB/wave: direct kernel
+    (128, 5, 40, 300, 100, 3, 5000),     # 2w+1 > 64 slots: direct kernel
     (64, 5, 3, 100, 25, 10, 4000),
     (96, 7, 4, 100, 25, 6, 4000),        # masked layout, MAXN = 10
     (2, 4, 3, 34, 20, 20, 5000),         # Karate shape
