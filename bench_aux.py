@@ -1,0 +1,191 @@
+"""Secondary benchmarks for the other hot-path rows (bench.py is the contract line for C3/O2).
+
+  --workload c2   BASELINE configs[1]: O1 (node_embeddings) on a synthetic SBM, 100 blocks x 1000
+                  nodes, ~1M edges, d=128, negative=5; a step = one Hogwild pass over all edges
+                  (come_sgns_o1); metric pair-updates/s; roofline HBM, (3+n)*d*4 B per pair.
+  --workload c4   BASELINE configs[3]: 1M nodes, K=50, d=128: the community-gradient pass
+                  (come_community_grad, iters=1) and the GMM responsibility pass
+                  (come_gmm_resp); each 2*V*K*d^2 flops; roofline = fp32 MFMA peak 157.3 TFLOP/s.
+Each prints one JSON line.  CPU baselines: the reference's own code on a bounded sample
+(O1: Cython train_o1 via oracle/_ref driven like Node2Vec.train; C4: the reference's numpy
+Community2Vec.train loop restated in oracle/oracle.py and sklearn predict_proba).
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA = f32 vector peak
+
+
+def log(*a):
+    print("[bench_aux]", *a, file=sys.stderr, flush=True)
+
+
+def timed(fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0), [a.elapsed_time(b) for a, b in ev]
+
+
+def ref_module():
+    import importlib.util
+    so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "training_sdg_inner*.so"))
+    if not so:
+        return None
+    spec = importlib.util.spec_from_file_location("training_sdg_inner", so[0])
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def c2(args):
+    import torch
+    import come_amd.training_sdg_inner as tsi
+    from come_amd.graph import sbm
+    from come_amd.model import Model
+    dev = torch.device("cuda", 0)
+    g = sbm(100, 1000, 0.016, 4.04e-5, seed=0)
+    np.random.seed(1234)
+    m = Model(g.degree_by_id(), size=args.dim, table_size=args.table_size, k=100, device=dev)
+    edges = torch.from_numpy(g.edges.astype(np.int32)).to(dev)
+    E = edges.shape[0]
+    np.random.seed(99)
+    seeds = [torch.from_numpy(tsi.draw_seeds(E).view(np.int64)).to(dev)
+             for _ in range(args.steps + args.warmup)]
+    it = iter(range(10 ** 9))
+
+    def step():
+        tsi.sgns_o1(m.node_embedding, edges, seeds[next(it) % len(seeds)], args.negative, m.table,
+                    0.2, tsi.MODE_HOGWILD)
+    el, ks = timed(step, args.steps, args.warmup)
+    pairs = 2 * E
+    n, d = args.negative, args.dim
+    bpp = (3 + n) * d * 4
+    avg = float(np.mean(ks)) / 1e3
+    cpu = None
+    ref = ref_module()
+    if ref is not None and not args.no_cpu_baseline:
+        node = m.node_embedding.cpu().numpy().copy()
+        table = m.table_host
+
+        class Vc(object):
+            __slots__ = ("index",)
+
+            def __init__(self, i):
+                self.index = i
+        sample = g.edges[:200000]
+        items = [[Vc(int(u)), Vc(int(v))] for u, v in sample]
+        work = np.zeros(d, np.float32)
+        t0 = time.time()
+        done = 0
+        # Node2Vec.train is GIL-bound (one Python call per edge): one thread
+        for e in items:
+            ref.train_o1(node, e, 0.2, n, table, py_size=d, py_work=work)
+            done += 1
+            if time.time() - t0 > args.cpu_seconds:
+                break
+        cel = time.time() - t0
+        cpu = {"value": 2 * done / cel, "unit": "pair-updates/s", "cores": 1,
+               "kind": "reference",
+               "sample": "reference Cython train_o1 (oracle/_ref), one call per edge as "
+                         "Node2Vec.train makes them (GIL-bound); %d edges in %.1fs" % (done, cel)}
+    print(json.dumps({
+        "metric": "O1 SGNS pair-updates/sec, SBM 100k nodes / 1M edges, d=128",
+        "value": pairs * args.steps / el, "unit": "pair-updates/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True, "dtype": "f32", "data": "synthetic SBM (seed 0)",
+        "config": {"workload": "configs[1]/C2: O1 over %d edges of a 100x1000 SBM, d=%d, "
+                               "negative=%d" % (E, d, n)},
+        "roofline": {"bound": "hbm", "achieved": bpp * pairs / avg / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": bpp * pairs / avg / 1e9 / HBM_PEAK_GBS,
+                     "bytes_per_pair": bpp, "avg_kernel_ms": avg * 1e3},
+        "cpu_baseline": cpu}))
+
+
+def c4(args):
+    import torch
+    from come_amd import community_embeddings as ce
+    from oracle import oracle as orc
+    dev = torch.device("cuda", 0)
+    V, K, d = args.nodes, args.k, args.dim
+    rng = np.random.RandomState(2)
+    x = torch.from_numpy(rng.standard_normal((V, d)).astype(np.float32)).to(dev)
+    A = rng.standard_normal((K, d, d)) / np.sqrt(d)
+    cov = np.einsum("kij,klj->kil", A, A) + np.eye(d)[None] * 0.5
+    inv = torch.from_numpy(np.linalg.inv(cov.astype(np.float32)).astype(np.float32)).to(dev)
+    mu = torch.from_numpy((rng.standard_normal((K, d)) * 0.5).astype(np.float32)).to(dev)
+    pi = torch.from_numpy(np.random.RandomState(3).dirichlet(np.ones(K), V).astype(np.float32)
+                          ).to(dev)
+    w = np.random.RandomState(4).dirichlet(np.ones(K))
+    pc, mp, ln = ce.gmm_resp_params(w, mu.cpu().numpy().astype(np.float64),
+                                    orc.precision_cholesky(cov), dev)
+    flops = 2.0 * V * K * d * d
+    x0 = x.clone()
+    el_g, ks_g = timed(lambda: ce.community_grad(x, pi, mu, inv, 0.01, 0.1, 1), args.steps,
+                       args.warmup)
+    el_r, ks_r = timed(lambda: ce.gmm_resp(x0, pc, mp, ln), args.steps, args.warmup)
+    tg, tr = float(np.mean(ks_g)) / 1e3, float(np.mean(ks_r)) / 1e3
+    cpu = None
+    if not args.no_cpu_baseline:
+        S = 4000
+        xs = x0[:S].cpu().numpy()
+        t0 = time.time()
+        orc.community_train(xs, pi[:S].cpu().numpy(), mu.cpu().numpy(), inv.cpu().numpy(),
+                            0.01, 0.1, 1)
+        cel = time.time() - t0
+        cpu = {"value": 2.0 * S * K * d * d / cel / 1e12, "unit": "TFLOP/s", "cores": 1,
+               "kind": "port",
+               "sample": "Community2Vec.train's numpy loop (community_embeddings.py:61-78, "
+                         "restated op for op in oracle/oracle.py) on %d of the %d rows: "
+                         "%.2fs -> %.0f s per full pass" % (S, V, cel, cel * V / S)}
+    print(json.dumps({
+        "metric": "community gradient + GMM responsibilities, 1M nodes K=50 d=128",
+        "value": flops / tg / 1e12, "unit": "TFLOP/s (community gradient pass)", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": tg * 1e3,
+        "higher_is_better": True, "dtype": "f32", "data": "synthetic N(0,1) rows, random SPD",
+        "config": {"workload": "configs[3]/C4: V=%d K=%d d=%d" % (V, K, d),
+                   "gmm_resp_ms": tr * 1e3, "gmm_resp_tflops": flops / tr / 1e12},
+        "roofline": {"bound": "mfma", "achieved": flops / tg / 1e12,
+                     "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": flops / tg / 1e12 / F32_MFMA_PEAK_TFLOPS,
+                     "flops_per_pass": flops, "avg_kernel_ms": tg * 1e3},
+        "cpu_baseline": cpu}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["c2", "c4"], required=True)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--table-size", type=int, default=100_000_000)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--k", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    {"c2": c2, "c4": c4}[args.workload](args)
+
+
+if __name__ == "__main__":
+    main()

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--variants", nargs="+", default=["default"])
     ap.add_argument("--warm-launches", type=int, default=2)
+    ap.add_argument("--table-size", type=int, default=100_000_000)
     args = ap.parse_args()
     import torch
     import come_amd.training_sdg_inner as tsi
@@ -39,7 +40,7 @@ def main():
     dev = torch.device("cuda", 0)
     g = chung_lu(args.nodes, 20.0, gamma=2.5, seed=1)
     np.random.seed(1234)
-    m = Model(g.degree_by_id(), size=args.dim, table_size=100_000_000, k=1, device=dev)
+    m = Model(g.degree_by_id(), size=args.dim, table_size=args.table_size, k=1, device=dev)
     walks = random_walks(g, 1, 80, seed=100, device=dev)[:args.walks].contiguous()
     np.random.seed(5678)
     seeds = torch.from_numpy(tsi.draw_seeds(args.walks).view(np.int64)).to(dev)
