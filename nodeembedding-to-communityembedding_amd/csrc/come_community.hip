@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "come_internal.h"
+#include "come_wave.h"
 
 namespace come {
 
@@ -138,6 +139,168 @@ __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
     }
 }
 
+// ---- MFMA version (d in {64, 128}) ------------------------------------------------------
+//
+// G = sum_k A_k M_k^T with A_k[i, :] = pi[i,k] (x_i - mu_k): one GEMM with a reduction of length
+// K*d whose A operand is generated on the fly.  v_mfma_f32_32x32x2_f32 (exact fp32 fmas, 64
+// cycles): lane (r, h) supplies A[row r][j = s + d/2 h] and B[j = s + d/2 h][col r] =
+// M_k[c0 + r][s + d/2 h], so a k-step pairs element s with element s + d/2.  A workgroup of 4
+// wavefronts owns 128 rows (32 per wavefront, CT = d/32 accumulator tiles each); M_k is staged
+// row-major with a 1-float pad (LD = d + 1: the B reads of a half-wave hit 32 distinct banks).
+// The epilogue moves the tile through LDS (C layout -> rows) to apply the clipped update and to
+// rebuild the A-layout registers for the next iteration.
+template <int D>
+__global__ void __launch_bounds__(256, 2) k_community_mfma(CommArgs a) {
+    constexpr int S = D / 2;  // k-steps per component
+    constexpr int CT = D / 32;
+    constexpr int LD = D + 1;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *Ms = sm;             // [D][LD]  (epilogue: [128][LD] row tile)
+    float *mus = sm + 128 * LD;  // [D]
+    const int tid = threadIdx.x;
+    const int wid = tid >> 6, lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t blk0 = (int64_t)blockIdx.x * 128;
+    const int64_t myrow = blk0 + wid * 32 + r;
+    const bool rowok = myrow < a.V;
+    float xa[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + q + S * h] : 0.0f;
+
+    for (int it = 0; it < a.iters; ++it) {
+        f32x16 acc[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
+        float p_next = rowok ? a.pi[myrow * a.K] : 0.0f;
+        for (int k = 0; k < a.K; ++k) {
+            __syncthreads();
+            const float *Mk = a.inv_cov + (int64_t)k * D * D;
+            for (int o = tid; o < D * D / 4; o += 256) {
+                const float4 v = reinterpret_cast<const float4 *>(Mk)[o];
+                const int c = (o * 4) / D, j = (o * 4) % D;
+                float *dst = Ms + c * LD + j;
+                dst[0] = v.x, dst[1] = v.y, dst[2] = v.z, dst[3] = v.w;
+            }
+            if (tid < D) mus[tid] = a.mu[k * D + tid];
+            const float p = p_next;
+            if (k + 1 < a.K) p_next = rowok ? a.pi[myrow * a.K + k + 1] : 0.0f;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < S; ++q) {
+                const float av = p * (xa[q] - mus[q + S * h]);
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    const float bv = Ms[(ct * 32 + r) * LD + q + S * h];
+                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ct], 0, 0, 0);
+                }
+            }
+        }
+        // epilogue: x -= lr * clip(coef * G, -5, 5), through a [128][LD] LDS row tile
+        __syncthreads();
+        float *X = Ms + wid * 32 * LD;  // this wavefront's 32 rows
+#pragma unroll
+        for (int q = 0; q < S; ++q) X[r * LD + q + S * h] = xa[q];
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's rows are in LDS
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+                float *px = X + row * LD + ct * 32 + r;
+                float g = acc[ct][e] * a.coef;
+                g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);
+                *px = *px - g * a.lr;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < S; ++q) xa[q] = X[r * LD + q + S * h];
+    }
+    if (rowok) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) a.x[myrow * D + q + S * h] = xa[q];
+    }
+}
+
+// GMM responsibilities on MFMA (d in {64, 128}): for each component the tile computes
+// Y = X P_k (A = the rows in the A layout of k_community_mfma, B = P_k staged [j][c]: a half-
+// wave reads 32 consecutive floats, conflict-free without padding), then sum_c (Y - mu P_k)^2
+// per row: squares summed over the CT column tiles in registers, then over the 32 columns of a
+// half-wave with the DPP / permlane16 stages 0-4.  Per-component log-probabilities go to
+// resp_out itself (scratch, one row per lane group), the softmax over k finishes in place.
+template <int D>
+__global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
+    constexpr int S = D / 2;
+    constexpr int CT = D / 32;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *Ps = sm;          // [D][D]
+    float *mps = Ps + D * D;  // [D]
+    const int tid = threadIdx.x;
+    const int wid = tid >> 6, lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t blk0 = (int64_t)blockIdx.x * 128;
+    const int64_t myrow = blk0 + wid * 32 + r;
+    const bool rowok = myrow < a.V;
+    float xa[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + q + S * h] : 0.0f;
+    for (int k = 0; k < a.K; ++k) {
+        __syncthreads();
+        const float4 *Pk = reinterpret_cast<const float4 *>(a.prec_chol + (int64_t)k * D * D);
+        for (int o = tid; o < D * D / 4; o += 256) reinterpret_cast<float4 *>(Ps)[o] = Pk[o];
+        if (tid < D) mps[tid] = a.mu_prec[k * D + tid];
+        __syncthreads();
+        f32x16 acc[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            const float av = xa[q];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const float bv = Ps[(q + S * h) * D + ct * 32 + r];
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ct], 0, 0, 0);
+            }
+        }
+        const float lnk = a.log_norm[k];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            float sq = 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const float y = acc[ct][e] - mps[ct * 32 + r];
+                sq = __builtin_fmaf(y, y, sq);
+            }
+            sq = reduce_stage<0>(sq);
+            sq = reduce_stage<1>(sq);
+            sq = reduce_stage<2>(sq);
+            sq = reduce_stage<3>(sq);
+            sq = reduce_stage<4>(sq);
+            const int64_t row = blk0 + wid * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (r == 0 && row < a.V) a.resp[row * a.K + k] = lnk - 0.5f * sq;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid < 128 && blk0 + tid < a.V) {
+        float *lp = a.resp + (blk0 + tid) * a.K;
+        float m = -INFINITY;
+        for (int k = 0; k < a.K; ++k) m = fmaxf(m, lp[k]);
+        float s = 0.0f;
+        for (int k = 0; k < a.K; ++k) s += expf(lp[k] - m);
+        const float lse = m + logf(s);
+        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+    }
+}
+
 }  // namespace come
 
 using namespace come;
@@ -153,6 +316,21 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     int rc = ensure_init(&dev);
     if (rc) return rc;
     CommArgs a{x, pi, mu, inv_cov, V, d, K, (float)((double)beta / (double)K), lr, iters};
+    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0) {
+        const unsigned grid = (unsigned)((V + 127) / 128);
+        const size_t lds = sizeof(float) * (size_t)(128 * (d + 1) + d);
+        void (*kern)(CommArgs) = d == 64 ? k_community_mfma<64> : k_community_mfma<128>;
+        static bool attr_m = false;
+        if (!attr_m) {
+            (void)hipFuncSetAttribute((const void *)k_community_mfma<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void *)k_community_mfma<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_m = true;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
+        return hip_error(hipGetLastError(), "k_community_mfma launch");
+    }
     const size_t lds = sizeof(float) * ((size_t)3 * kTR * d + (size_t)d * d);
     const unsigned grid = (unsigned)((V + kTR - 1) / kTR);
     static bool attr = false;
@@ -177,6 +355,21 @@ extern "C" int come_gmm_resp(const float *x, int64_t V, int d, const float *prec
     int rc = ensure_init(&dev);
     if (rc) return rc;
     RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, V, d, K};
+    if ((d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0) {
+        const unsigned grid = (unsigned)((V + 127) / 128);
+        const size_t lds = sizeof(float) * (size_t)(d * d + d);
+        void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_mfma<64> : k_gmm_resp_mfma<128>;
+        static bool attr_m = false;
+        if (!attr_m) {
+            (void)hipFuncSetAttribute((const void *)k_gmm_resp_mfma<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void *)k_gmm_resp_mfma<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_m = true;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
+        return hip_error(hipGetLastError(), "k_gmm_resp_mfma launch");
+    }
     const size_t lds = sizeof(float) * ((size_t)kTR * d + (size_t)d * d + kTR * 64 + kTR);
     const unsigned grid = (unsigned)((V + kTR - 1) / kTR);
     static bool attr = false;

@@ -305,6 +305,26 @@ def test_community_grad_vs_golden():
                                    err_msg=name)
 
 
+@pytest.mark.parametrize("d,V,K,iters", [(64, 1000, 7, 3), (128, 777, 5, 2), (128, 300, 1, 1),
+                                          (96, 200, 3, 2)])
+def test_community_grad_vs_oracle(d, V, K, iters):
+    """MFMA path (d = 64, 128; ragged row tiles) and VALU path (d = 96) against the numpy
+    restatement of community_embeddings.py:61-78: fp32 contractions in another order,
+    rtol/atol 2e-5; the clip at +-5 is exercised (beta large)."""
+    rng = np.random.RandomState(d + V)
+    x0 = rng.normal(size=(V, d)).astype(np.float32)
+    A = rng.normal(size=(K, d, d)) / np.sqrt(d)
+    cov = np.einsum("kij,klj->kil", A, A) + np.eye(d)[None] * 0.5
+    inv = np.linalg.inv(cov.astype(np.float32)).astype(np.float32)
+    mu = rng.normal(size=(K, d)).astype(np.float32)
+    pi = rng.dirichlet(np.ones(K), V).astype(np.float32)
+    for beta in (0.05, 40.0):
+        x = dev(x0)
+        ce.community_grad(x, dev(pi), dev(mu), dev(inv), beta, 0.1, iters)
+        ref = orc.community_train(x0, pi, mu, inv, beta, 0.1, iters)
+        np.testing.assert_allclose(x.cpu().numpy(), ref, rtol=2e-5, atol=2e-5)
+
+
 def test_gmm_resp_vs_golden():
     z = np.load(os.path.join(GOLDEN, "gmm_resp.npz"))
     for name in z["names"]:
