@@ -127,6 +127,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--all-ranks-device0", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (needs --dist-backend gloo)")
     args = ap.parse_args()
 
     import torch
@@ -141,10 +145,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    if args.all_ranks_device0:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     # ---- workload: C3 (same graph on every rank; walks sharded by rank) ----
     t0 = time.time()
@@ -276,8 +285,9 @@ def main():
             "walks_per_step_per_gpu": B,
             "pairs_per_step_per_gpu": pairs_rank_step,
             "sync_every_steps": args.sync_every if world > 1 else None,
-            "parallelism": "walk-shard dp%d + delta all-reduce (RCCL)" % world if world > 1
-            else "single GPU, Hogwild over walks",
+            "parallelism": "walk-shard dp%d + delta all-reduce (%s)" % (
+                world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend)
+            if world > 1 else "single GPU, Hogwild over walks",
         },
         "roofline": {
             "bound": "hbm",
