@@ -6,6 +6,12 @@
   --workload c4   BASELINE configs[3]: 1M nodes, K=50, d=128: the community-gradient pass
                   (come_community_grad, iters=1) and the GMM responsibility pass
                   (come_gmm_resp); each 2*V*K*d^2 flops; roofline = fp32 MFMA peak 157.3 TFLOP/s.
+  --workload walks  SURVEY.md §8f row 1, the producer of C3's input: one corpus pass over the C3
+                  graph (1M-node power law, every node starts one walk, length 80) on the HIP
+                  walker (come_random_walks); metric walk-steps/s; roofline HBM with 24 B per step
+                  (rowptr pair + one col entry + the written entry).  CPU baseline: the exact
+                  CPython-stream walker (come_walks_reference, native restatement of
+                  graph_utils.build_deepwalk_corpus) on host threads.
 Each prints one JSON line.  CPU baselines: the reference's own code on a bounded sample
 (O1: Cython train_o1 via oracle/_ref driven like Node2Vec.train; C4: the reference's numpy
 Community2Vec.train loop restated in oracle/oracle.py and sklearn predict_proba).
@@ -171,9 +177,58 @@ def c4(args):
         "cpu_baseline": cpu}))
 
 
+def walks(args):
+    import random
+    import torch
+    from come_amd import graph_utils as gu
+    from come_amd.graph import chung_lu
+    dev = torch.device("cuda", 0)
+    g = chung_lu(args.nodes, 20.0, gamma=2.5, seed=1)
+    L = 80
+    rowptr = torch.from_numpy(g.rowptr).to(dev)
+    col = torch.from_numpy(g.col.astype(np.int32)).to(dev)
+    starts = torch.randperm(g.V, device=dev).int()
+    out = torch.empty((g.V, L), dtype=torch.int32, device=dev)
+    it = iter(range(10 ** 9))
+
+    def step():
+        gu.device_walks(rowptr, col, starts, L, alpha=0.0, seed=next(it), out=out)
+    el, ks = timed(step, args.steps, args.warmup)
+    steps_per_launch = float((out >= 0).sum().item() - g.V)  # moves (the start is not a step)
+    avg = float(np.mean(ks)) / 1e3
+    bps = 24
+    cpu = None
+    if not args.no_cpu_baseline:
+        Gh = gu.Graph(np.arange(1, g.V + 1), g.rowptr, g.col.astype(np.int32), g.degree,
+                      np.zeros((0, 2), np.int32))
+        threads = min(16, os.cpu_count() or 1)
+        t0 = time.time()  # one full pass per stream, streams on parallel threads
+        w = gu._corpus(Gh, [1] * threads, L, 0.0, [random.Random(s) for s in range(threads)],
+                       threads=threads)
+        cel = time.time() - t0
+        moves = float((w >= 0).sum() - w.shape[0])
+        cpu = {"value": moves / cel, "unit": "walk-steps/s", "cores": threads, "kind": "port",
+               "sample": "exact CPython-stream walker (come_walks_reference, restating "
+                         "graph_utils.build_deepwalk_corpus + __random_walk__), %d streams x one "
+                         "pass of %d walks on %d host threads: %.1fs" % (threads, g.V, threads,
+                                                                        cel)}
+    print(json.dumps({
+        "metric": "random-walk steps/sec, 1M-node power-law graph, walk length 80",
+        "value": steps_per_launch * args.steps / el, "unit": "walk-steps/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True, "dtype": "int32", "data": "synthetic Chung-Lu (seed 1)",
+        "config": {"workload": "walk corpus pass: V=%d, E=%d, L=%d, alpha=0" % (
+            g.V, g.num_edges, L)},
+        "roofline": {"bound": "hbm", "achieved": bps * steps_per_launch / avg / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": bps * steps_per_launch / avg / 1e9 / HBM_PEAK_GBS,
+                     "bytes_per_step": bps, "avg_kernel_ms": avg * 1e3},
+        "cpu_baseline": cpu}))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c4"], required=True)
+    ap.add_argument("--workload", choices=["c2", "c4", "walks"], required=True)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--dim", type=int, default=128)
@@ -184,7 +239,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    {"c2": c2, "c4": c4}[args.workload](args)
+    {"c2": c2, "c4": c4, "walks": walks}[args.workload](args)
 
 
 if __name__ == "__main__":

@@ -98,6 +98,66 @@ int come_community_grad(float *x, int64_t V, int d, const float *pi, const float
 int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
                   const float *log_norm, int K, float *resp_out, void *stream);
 
+/* ---- Random walks: the producer of train_o2's input (utils/graph_utils.py) ----
+ * Graphs are CSR over node POSITIONS 0..V-1 in networkx order (see come_graph_from_edges):
+ * rowptr int64 [V+1], col int32 [rowptr[V]] (neighbours in adjacency order).  `emit` (optional,
+ * int32 [V]) maps a position to the value written into a walk (e.g. the node's Vocab.index row);
+ * NULL writes positions.  Walk rows are [P x path_length] int32, -1 after a walk ends. */
+
+/* Device walker, same distribution as __random_walk__ (graph_utils.py:20-46): from the current
+ * node jump back to the walk's start with probability alpha, else move to a uniform neighbour;
+ * a node without neighbours ends the walk.  starts: device int32 [P] positions (one walk per
+ * start; build_deepwalk_corpus_iter :187-192 starts one walk at every node per pass, in shuffled
+ * order).  Random stream: Philox-4x32-10 keyed by `seed`, counter (walk_offset + walk, step) --
+ * independent of launch shape, not the reference's CPython stream.  rowptr/col/emit/out are
+ * device pointers. */
+int come_random_walks(const int64_t *rowptr, const int32_t *col, int64_t V,
+                      const int32_t *starts, int64_t P, int path_length, float alpha,
+                      uint64_t seed, int64_t walk_offset, const int32_t *emit, int32_t *out,
+                      void *stream);
+
+/* Host, exact: build_deepwalk_corpus_iter (graph_utils.py:187-192) with the reference's own
+ * random stream.  n_streams independent CPython random.Random streams (one per walk file of
+ * write_walks_to_disk :122-146); stream s writes paths_per_stream[s] passes of V walks, streams
+ * concatenated in order.  states: [n_streams x 625] uint32 = random.Random.getstate()[1] (624
+ * MT19937 words + position), advanced in place (setstate() them back to continue the Python
+ * streams).  Streams run on up to `threads` host threads.  All pointers are host pointers. */
+int come_walks_reference(const int64_t *rowptr, const int32_t *col, int64_t V, int n_streams,
+                         const int32_t *paths_per_stream, uint32_t *states, int path_length,
+                         double alpha, const int32_t *emit, int threads, int32_t *out);
+
+/* Host: random.Random(seed).getstate()[1] for 0 <= seed < 2^64 (CPython init_by_array). */
+int come_pyrandom_seed(uint64_t seed, uint32_t *state625);
+
+/* Host: `count` draws from a CPython random.Random state (advanced in place): kind 0 =
+ * random(), kind 1 = _randbelow(arg) (arg <= 2^32).  Test hook for the restated stream. */
+int come_pyrandom_draw(uint32_t *state625, int kind, uint64_t arg, int64_t count, double *out);
+
+/* Host: nx.Graph().add_edges_from(edges) (graph_utils.py:60-69) in networkx order.
+ * edges int64 [E x 2] node ids in file order.  Outputs (capacities 2E, 2E+1 for rowptr):
+ * node_ids[V] = list(G.nodes()) (first appearance), rowptr/col = adjacency in insertion order
+ * (duplicates dropped, a self-loop listed once), degree[V] = G.degree() (self-loop counts 2),
+ * edge_pos [E' x 2] = G.edges() as positions, in networkx order. */
+int come_graph_from_edges(const int64_t *edges, int64_t E, int64_t *node_ids, int64_t *V_out,
+                          int64_t *rowptr, int32_t *col, int64_t *degree, int32_t *edge_pos,
+                          int64_t *E_out);
+
+/* ---- Text formats (host) ----
+ * Integer rows (edge lists graph_utils.py:49-109, walk files :112-120/:149-154): one row per
+ * line of whitespace-separated integers; '#' lines and blank lines skipped.  With rows == NULL
+ * only counts (nrows_out, max_tokens_out); else fills rows [cap_rows x width], -1 padded. */
+int come_read_int_rows(const char *path, int64_t *rows, int64_t cap_rows, int width,
+                       int64_t *nrows_out, int *max_tokens_out);
+/* Writes rows [nrows x width] one per line, space separated, each ending at its first
+ * negative entry (the walk-file format of _write_walks_to_disk :117-118). */
+int come_write_int_rows(const char *path, const int64_t *rows, int64_t nrows, int width,
+                        int append);
+/* IO_utils.save_embedding (:49-62): "<first_id + i>\t<v1> <v2> ...\n", each value exactly as
+ * numpy's str(np.float32) prints it.  emb: host fp32 [V x d]. */
+int come_save_embedding(const char *path, const float *emb, int64_t V, int d, int64_t first_id);
+/* str(np.float32(x)) into out32 (NUL-terminated); returns its length. */
+int come_format_f32(float x, char *out32);
+
 /* ---- Tuning ----
  * Process-wide launch knobs for experiments (0 = automatic): "o2_kernel" (1 direct, 2 ring),
  * "o2_blocks_per_cu", "o2_waves_per_block", "o2_plain_writeback" (1 = Hogwild with plain-store

@@ -15,7 +15,10 @@ MODE_SEQUENTIAL = 1
 # Every symbol include/come.h declares (checked by tests/test_capi.py).
 SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_fast_version", "come_sgns_o2", "come_sgns_o1", "come_community_grad",
-           "come_gmm_resp", "come_make_table", "come_count_o2_pairs", "come_set_option")
+           "come_gmm_resp", "come_make_table", "come_count_o2_pairs", "come_set_option",
+           "come_random_walks", "come_walks_reference", "come_pyrandom_seed",
+           "come_pyrandom_draw", "come_graph_from_edges", "come_read_int_rows",
+           "come_write_int_rows", "come_save_embedding", "come_format_f32")
 
 _lib = None
 
@@ -54,6 +57,16 @@ def lib():
     L.come_count_o2_pairs.argtypes = [P, i64, i32, i32]
     L.come_count_o2_pairs.restype = i64
     L.come_set_option.argtypes = [ctypes.c_char_p, i32]
+    cp = ctypes.c_char_p
+    L.come_random_walks.argtypes = [P, P, i64, P, i64, i32, f32, u64, i64, P, P, P]
+    L.come_walks_reference.argtypes = [P, P, i64, i32, P, P, i32, f64, P, i32, P]
+    L.come_pyrandom_seed.argtypes = [u64, P]
+    L.come_pyrandom_draw.argtypes = [P, i32, u64, i64, P]
+    L.come_graph_from_edges.argtypes = [P, i64, P, P, P, P, P, P, P]
+    L.come_read_int_rows.argtypes = [cp, P, i64, i32, P, P]
+    L.come_write_int_rows.argtypes = [cp, P, i64, i32, i32]
+    L.come_save_embedding.argtypes = [cp, P, i64, i32, i64]
+    L.come_format_f32.argtypes = [f32, cp]
     if L.come_abi_version() != 1:
         raise ComeError("libcome.so ABI version mismatch")
     _lib = L

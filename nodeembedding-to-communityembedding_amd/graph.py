@@ -4,8 +4,9 @@ Reference counterparts: ``utils/graph_utils.py`` -- ``load_adjacencylist`` (:72-
 truncated walk with restart ``__random_walk__`` (:20-46) and ``build_deepwalk_corpus_iter``
 (:187-192: per pass, shuffle the node list and start one walk at every node).  Walks here are
 generated for whole batches at once on the device from a CSR adjacency (uniform neighbour choice,
-restart probability alpha, a walk stops at a node without neighbours) -- same distribution as the
-reference walker, not the same random stream (the reference uses Python's random.Random).
+restart probability alpha, a walk stops at a node without neighbours; HIP kernel
+come_random_walks) -- same distribution as the reference walker, not the same random stream.  The
+reference's exact stream (CPython random.Random) is graph_utils.build_deepwalk_corpus.
 
 Synthetic generators for the benchmark configurations: ``chung_lu`` (power-law
 expected degrees) and ``sbm`` (stochastic block model).  Node ids are 1..V (row = id - 1).
@@ -102,33 +103,17 @@ def sbm(blocks, block_size, p_in, p_out, seed=0):
 def random_walks(g, num_paths, path_length, alpha=0.0, seed=0, device="cuda", starts=None):
     """Walks [num_paths * V, path_length] of ROW indices (int32 tensor on `device`), -1 after a
     walk stops.  Per pass the start nodes are a fresh permutation of all nodes (graph_utils.py:
-    187-192); each step moves to a uniformly chosen neighbour, or with probability alpha back to
-    the walk's first node (:36-43)."""
+    187-192); the walks themselves come from the HIP walker (come_random_walks: uniform
+    neighbour, restart to the first node with probability alpha, Philox stream keyed by seed)."""
     import torch
-    gen = torch.Generator(device=device)
+    from .graph_utils import device_walks
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
     gen.manual_seed(seed)
-    rowptr = torch.from_numpy(g.rowptr).to(device)
-    col = torch.from_numpy(g.col.astype(np.int64)).to(device)
-    deg = rowptr[1:] - rowptr[:-1]
+    rowptr = torch.from_numpy(g.rowptr).to(dev)
+    col = torch.from_numpy(g.col.astype(np.int32)).to(dev)
     if starts is None:
-        starts = torch.cat([torch.randperm(g.V, generator=gen, device=device)
+        starts = torch.cat([torch.randperm(g.V, generator=gen, device=dev)
                             for _ in range(num_paths)])
-    else:
-        starts = torch.as_tensor(starts, device=device).long()
-    P = starts.numel()
-    out = torch.full((P, path_length), -1, dtype=torch.int32, device=device)
-    cur = starts.clone()
-    alive = torch.ones(P, dtype=torch.bool, device=device)
-    out[:, 0] = cur.int()
-    for t in range(1, path_length):
-        dc = deg[cur]
-        alive &= dc > 0
-        r = torch.rand(P, generator=gen, device=device)
-        pick = (r * dc.double().clamp(min=1).float()).long().clamp(max=(dc - 1).clamp(min=0))
-        nxt = col[(rowptr[cur] + pick).clamp(max=max(col.numel() - 1, 0))]
-        if alpha > 0:
-            back = torch.rand(P, generator=gen, device=device) < alpha
-            nxt = torch.where(back, starts, nxt)
-        cur = torch.where(alive, nxt, cur)
-        out[:, t] = torch.where(alive, cur.int(), torch.full_like(cur.int(), -1))
-    return out
+    starts = torch.as_tensor(starts, device=dev).to(torch.int32).contiguous()
+    return device_walks(rowptr, col, starts, path_length, alpha=alpha, seed=seed)

@@ -1,7 +1,8 @@
 """Label / embedding text formats of the reference ``utils/IO_utils.py``.
 
 ``load_ground_true`` (:18-47), ``save_ground_true`` (:8-16), ``save_embedding`` (:49-62, one line
-per node: ``<node_id>\\t<v1> <v2> ...`` with 1-based ids), ``load_embedding`` (:64-80).  The
+per node: ``<node_id>\\t<v1> <v2> ...`` with 1-based ids; native writer, byte-identical to the
+reference's str(np.float32) output), ``load_embedding`` (:64-80).  The
 reference's pickle ``save``/``load`` (:82-105) are not reproduced (unsafe; Model.save replaces
 them).
 """
@@ -38,12 +39,16 @@ def _to_numpy(embeddings):
 
 
 def save_embedding(embeddings, file_name, path='data'):
+    """IO_utils.save_embedding (:49-62), written natively (come_save_embedding): the same bytes
+    as the reference's str(np.float32) per value, for fp32 tables (host or device)."""
+    from . import _lib
     full_path = path_join(path, file_name + '.txt')
     makedirs(dirname(full_path), exist_ok=True)
-    emb = _to_numpy(embeddings)
-    with open(full_path, 'w') as f:
-        for node_id, embed in enumerate(emb):
-            f.write(str(node_id + 1) + '\t' + " ".join([str(val) for val in embed]) + '\n')
+    emb = np.ascontiguousarray(_to_numpy(embeddings), dtype=np.float32)
+    if emb.ndim != 2:
+        raise ValueError("embeddings must be 2-D")
+    _lib.check(_lib.lib().come_save_embedding(full_path.encode(), _lib.ptr(emb), emb.shape[0],
+                                              emb.shape[1], 1), "come_save_embedding")
 
 
 def load_embedding(file_name, path='data', ext=".txt"):

@@ -11,6 +11,11 @@ only as the checker.  The product package (come_amd) never imports it.
   for covariance_type='full' (sklearn 1.7.2 `_estimate_log_gaussian_prob` +
   `_estimate_weighted_log_prob` + logsumexp normalisation), called by
   community_embeddings.py:37, plus the fp32 np.linalg.inv of :36.
+* Graph + walks: pure-Python restatement of utils/graph_utils.py -- networkx's add_edges_from /
+  nodes / edges / degree order (graph_utils.py:60-69) and build_deepwalk_corpus (:172-185) +
+  __random_walk__ (:20-46) driven by CPython's own random.Random (the reference's RNG), for small
+  graphs.  Pinned against tests/golden/walks.npz (make_golden_walks.py, produced by the
+  reference's graph_utils itself).
 
 Parity pin: tests/test_oracle_golden.py checks every function here against the fixtures that
 tests/golden/make_golden.py produced from the reference itself.
@@ -161,3 +166,64 @@ def gmm_log_resp(X, weights, means, cov):
 
 def gmm_predict_proba(X, weights, means, cov):
     return np.exp(gmm_log_resp(X, weights, means, cov))
+
+
+# ---- graph_utils (graph_utils.py:20-46, 60-69, 172-185) -------------------------------------
+def nx_graph(edges):
+    """networkx.Graph().add_edges_from(edges) as plain dicts: {node: {nbr: None}} in insertion
+    order (first appearance of a node, first insertion of a neighbour)."""
+    adj = {}
+    for u, v in edges:
+        u, v = int(u), int(v)
+        adj.setdefault(u, {})
+        adj.setdefault(v, {})
+        adj[u][v] = None
+        adj[v][u] = None
+    return adj
+
+
+def nx_to_undirected(adj):
+    """nx.Graph.to_undirected(): add_edges_from((u, v) for u in adj for v in adj[u]) into a
+    fresh graph that already holds every node in order."""
+    new = {n: {} for n in adj}
+    for u, nbrs in adj.items():
+        for v in nbrs:
+            new[u][v] = None
+            new[v][u] = None
+    return new
+
+
+def nx_edges(adj):
+    """np.array(G.edges()) order: nodes in order, neighbours not yet visited."""
+    seen, out = set(), []
+    for n, nbrs in adj.items():
+        for m in nbrs:
+            if m not in seen:
+                out.append((n, m))
+        seen.add(n)
+    return out
+
+
+def nx_degree(adj):
+    return [len(nbrs) + (1 if n in nbrs else 0) for n, nbrs in adj.items()]
+
+
+def deepwalk_corpus(adj, num_paths, path_length, alpha, rand):
+    """build_deepwalk_corpus with start=node for every node per pass; returns lists of ids."""
+    nodes = list(adj)
+    walks = []
+    for _ in range(num_paths):
+        rand.shuffle(nodes)
+        for node in nodes:
+            path = [node]
+            while len(path) < path_length:
+                nb = list(adj[path[-1]])
+                if len(nb) > 0:
+                    if rand.random() >= alpha:
+                        path.append(rand.choice(nb))
+                    else:
+                        path.append(path[0])
+                else:
+                    break
+            walks.append(path)
+    return walks
