@@ -150,6 +150,20 @@ def c4(args):
                        args.warmup)
     el_r, ks_r = timed(lambda: ce.gmm_resp(x0, pc, mp, ln), args.steps, args.warmup)
     tg, tr = float(np.mean(ks_g)) / 1e3, float(np.mean(ks_r)) / 1e3
+    # one GMM EM iteration (come_amd.gmm: E-step kernel + means GEMM + scatter kernel + K
+    # Cholesky factorisations), and the M-step scatter kernel alone
+    from come_amd import gmm
+    gm = gmm.GaussianMixture(K, reg_covar=1e-5)
+    t64 = lambda a: torch.as_tensor(np.asarray(a, np.float64), device=dev)  # noqa: E731
+    gm._set_params(t64(w), mu.double(), t64(cov))
+    resp0 = pi.contiguous()
+
+    def em_iter():
+        resp, _ = gmm.estep(x0, gm._e_pc, gm._e_mp, gm._e_ln)
+        gm._set_params(*gm._m_step(x0, resp))
+    el_e, ks_e = timed(em_iter, args.steps, args.warmup)
+    el_s, ks_s = timed(lambda: gmm.scatter(x0, resp0, mu), args.steps, args.warmup)
+    te, ts = float(np.mean(ks_e)) / 1e3, float(np.mean(ks_s)) / 1e3
     cpu = None
     if not args.no_cpu_baseline:
         S = 4000
@@ -163,13 +177,33 @@ def c4(args):
                "sample": "Community2Vec.train's numpy loop (community_embeddings.py:61-78, "
                          "restated op for op in oracle/oracle.py) on %d of the %d rows: "
                          "%.2fs -> %.0f s per full pass" % (S, V, cel, cel * V / S)}
+        from sklearn.mixture import GaussianMixture as SkGMM
+        S2 = 20000
+        Xs = x0[:S2].cpu().numpy()
+        sk = SkGMM(K, covariance_type="full", reg_covar=1e-5, max_iter=1, tol=0.0,
+                   weights_init=w, means_init=mu.cpu().numpy().astype(np.float64),
+                   precisions_init=np.linalg.inv(cov), random_state=0)
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            sk._check_parameters(Xs)
+            sk._initialize_parameters(Xs, np.random.RandomState(0))
+            t0 = time.time()
+            lpn, lr = sk._e_step(Xs)
+            sk._m_step(Xs, lr)
+            sel = time.time() - t0
+        cpu["gmm_em_iteration_sample"] = (
+            "sklearn GaussianMixture E+M step (community_embeddings.py:27's estimator) on %d "
+            "rows: %.2fs -> %.1f s per full-size iteration" % (S2, sel, sel * V / S2))
     print(json.dumps({
         "metric": "community gradient + GMM responsibilities, 1M nodes K=50 d=128",
         "value": flops / tg / 1e12, "unit": "TFLOP/s (community gradient pass)", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": tg * 1e3,
         "higher_is_better": True, "dtype": "f32", "data": "synthetic N(0,1) rows, random SPD",
         "config": {"workload": "configs[3]/C4: V=%d K=%d d=%d" % (V, K, d),
-                   "gmm_resp_ms": tr * 1e3, "gmm_resp_tflops": flops / tr / 1e12},
+                   "gmm_resp_ms": tr * 1e3, "gmm_resp_tflops": flops / tr / 1e12,
+                   "gmm_scatter_ms": ts * 1e3, "gmm_scatter_tflops": flops / ts / 1e12,
+                   "gmm_em_iteration_ms": te * 1e3},
         "roofline": {"bound": "mfma", "achieved": flops / tg / 1e12,
                      "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": flops / tg / 1e12 / F32_MFMA_PEAK_TFLOPS,

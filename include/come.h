@@ -98,6 +98,21 @@ int come_community_grad(float *x, int64_t V, int d, const float *pi, const float
 int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
                   const float *log_norm, int K, float *resp_out, void *stream);
 
+/* ---- GMM EM fit (replaces GaussianMixture.fit, community_embeddings.py:27; sklearn
+ * BaseMixture.fit_predict / _e_step / _m_step for covariance_type='full') ----
+ * E-step: come_gmm_resp plus lse_out [V] = per-row log sum_k exp(log w_k + log N(x; mu_k, S_k))
+ * (the mean of lse_out is sklearn's log_prob_norm / lower bound). */
+int come_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
+                   const float *log_norm, int K, float *resp_out, float *lse_out, void *stream);
+
+/* M-step scatter matrices: scatter_out [K x d x d] = sum_i resp[i,k] (x_i - means_k)
+ * (x_i - means_k)^T (device fp32; covariance_k = scatter_k / nk_k + reg_covar I, sklearn
+ * _estimate_gaussian_covariances_full).  Rows are split into `chunks` partial sums reduced in a
+ * fixed order (deterministic); scratch: device fp32 [chunks x K x d x d] (unused when
+ * chunks == 1).  d <= 128. */
+int come_gmm_scatter(const float *x, int64_t V, int d, const float *resp, const float *means,
+                     int K, int chunks, float *scratch, float *scatter_out, void *stream);
+
 /* ---- Random walks: the producer of train_o2's input (utils/graph_utils.py) ----
  * Graphs are CSR over node POSITIONS 0..V-1 in networkx order (see come_graph_from_edges):
  * rowptr int64 [V+1], col int32 [rowptr[V]] (neighbours in adjacency order).  `emit` (optional,

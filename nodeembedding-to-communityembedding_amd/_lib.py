@@ -18,7 +18,8 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_gmm_resp", "come_make_table", "come_count_o2_pairs", "come_set_option",
            "come_random_walks", "come_walks_reference", "come_pyrandom_seed",
            "come_pyrandom_draw", "come_graph_from_edges", "come_read_int_rows",
-           "come_write_int_rows", "come_save_embedding", "come_format_f32")
+           "come_write_int_rows", "come_save_embedding", "come_format_f32",
+           "come_gmm_estep", "come_gmm_scatter")
 
 _lib = None
 
@@ -53,6 +54,8 @@ def lib():
     L.come_sgns_o1.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, P]
     L.come_community_grad.argtypes = [P, i64, i32, P, P, P, i32, f32, f32, i32, P]
     L.come_gmm_resp.argtypes = [P, i64, i32, P, P, P, i32, P, P]
+    L.come_gmm_estep.argtypes = [P, i64, i32, P, P, P, i32, P, P, P]
+    L.come_gmm_scatter.argtypes = [P, i64, i32, P, P, i32, i32, P, P, P]
     L.come_make_table.argtypes = [P, i64, P, u64, f64]
     L.come_count_o2_pairs.argtypes = [P, i64, i32, i32]
     L.come_count_o2_pairs.restype = i64

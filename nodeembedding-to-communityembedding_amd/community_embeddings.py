@@ -1,17 +1,18 @@
 """Community embedding trainer -- reference: ADSCModel/community_embeddings.py.
 
-``Community2Vec(model, lr, reg_covar)``:
-  * ``fit(model)`` (:20-37): fits sklearn's GaussianMixture(n_components=k, covariance_type=
-    'full', n_init=10, reg_covar) on the host exactly as the reference does (unseeded: it draws from
-    the global numpy RNG), stores centroid / covariance_mat (fp32 casts) and inv_covariance_mat
-    (np.linalg.inv of the fp32 covariances, :36) on the GPU, and computes the responsibilities pi
-    (:37, predict_proba) on the GPU with come_gmm_resp.
+``Community2Vec(model, lr, reg_covar, gmm_backend="gpu")``:
+  * ``fit(model)`` (:20-37): fits a GaussianMixture(n_components=k, covariance_type='full',
+    n_init=10, reg_covar) -- by default the GPU EM of come_amd.gmm (MFMA E-step and M-step
+    kernels, k-means init; unseeded like the reference's: the init draws its seed from the global
+    numpy RNG), or with ``gmm_backend="sklearn"`` sklearn's own estimator on the host exactly as
+    the reference does -- then stores centroid / covariance_mat (fp32 casts) and
+    inv_covariance_mat (the inverse of the fp32 covariances, :36) on the GPU, and computes the
+    responsibilities pi (:37, predict_proba) on the GPU with come_gmm_resp.
   * ``train(nodes, model, beta, chunksize, iter)`` (:61-78): the full-batch community gradient
     x -= lr * clip((beta/K) sum_k pi_ik inv_cov_k (x_i - mu_k), +-5), ``iter`` times, on the GPU
     (come_community_grad).  Every row's gradient depends only on that row (:65 snapshot), so rows
     outside ``nodes`` are left untouched by gathering/scattering the selected rows.
   * ``responsibilities(model)``: predict_proba of the fitted mixture on the current embedding.
-The GMM EM fit itself stays on the host in this round.
 """
 import logging as log
 
@@ -58,23 +59,32 @@ def community_grad(x, pi, mu, inv_cov, beta, lr, iters):
 
 
 class Community2Vec(object):
-    def __init__(self, model, lr, reg_covar=0):
-        from sklearn import mixture
+    def __init__(self, model, lr, reg_covar=0, gmm_backend="gpu"):
         self.lr = lr
-        self.g_mixture = mixture.GaussianMixture(n_components=model.k, reg_covar=reg_covar,
-                                                 covariance_type='full', n_init=10)
+        self.gmm_backend = gmm_backend
+        if gmm_backend == "gpu":
+            from .gmm import GaussianMixture
+            self.g_mixture = GaussianMixture(n_components=model.k, reg_covar=reg_covar,
+                                             covariance_type='full', n_init=10)
+        elif gmm_backend == "sklearn":
+            from sklearn import mixture
+            self.g_mixture = mixture.GaussianMixture(n_components=model.k, reg_covar=reg_covar,
+                                                     covariance_type='full', n_init=10)
+        else:
+            raise ValueError("gmm_backend must be 'gpu' or 'sklearn'")
 
     def fit(self, model):
         import torch
         log.info("Fitting: {} communities".format(model.k))
-        X = model.node_embedding.detach().cpu().numpy()
-        self.g_mixture.fit(X)
         dev = model.node_embedding.device
-        cov32 = self.g_mixture.covariances_.astype(np.float32)
+        if self.gmm_backend == "gpu":
+            self.g_mixture.fit(model.node_embedding)
+        else:
+            self.g_mixture.fit(model.node_embedding.detach().cpu().numpy())
+        cov32 = torch.from_numpy(self.g_mixture.covariances_.astype(np.float32)).to(dev)
         model.centroid = torch.from_numpy(self.g_mixture.means_.astype(np.float32)).to(dev)
-        model.covariance_mat = torch.from_numpy(cov32).to(dev)
-        model.inv_covariance_mat = torch.from_numpy(
-            np.linalg.inv(cov32).astype(np.float32)).to(dev)
+        model.covariance_mat = cov32
+        model.inv_covariance_mat = torch.linalg.inv(cov32).contiguous()  # :36, fp32 inverse
         model.pi = self.responsibilities(model)
 
     def responsibilities(self, model):

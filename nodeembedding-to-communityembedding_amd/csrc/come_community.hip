@@ -95,6 +95,7 @@ struct RespArgs {
     const float *mu_prec;
     const float *log_norm;
     float *resp;
+    float *lse;  // optional [V]: log sum_k exp(weighted log prob) per row (EM's log-likelihood)
     int64_t V;
     int d;
     int K;
@@ -136,6 +137,7 @@ __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
         for (int k = 0; k < a.K; ++k) s += expf(LP[r * 64 + k] - m);
         const float lse = m + logf(s);
         for (int k = 0; k < a.K; ++k) a.resp[(r0 + r) * a.K + k] = expf(LP[r * 64 + k] - lse);
+        if (a.lse) a.lse[r0 + r] = lse;
     }
 }
 
@@ -298,7 +300,146 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
         for (int k = 0; k < a.K; ++k) s += expf(lp[k] - m);
         const float lse = m + logf(s);
         for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+        if (a.lse) a.lse[blk0 + tid] = lse;
     }
+}
+
+
+// ---- GMM M-step scatter matrices -------------------------------------------------------------
+//
+// S_k = sum_i resp[i,k] (x_i - mu_k)(x_i - mu_k)^T, the numerator of sklearn's full covariance
+// (_estimate_gaussian_covariances_full: np.dot(resp[:, k] * diff.T, diff) / nk[k]), 2 V K d^2
+// flops per M-step.  Workgroup (k, chunk): rows of the chunk are staged through LDS in blocks of
+// kCovRB samples, centred on mu_k, with their weights; the reduction over samples is the MFMA
+// k-dimension (v_mfma_f32_32x32x2_f32: lane (r, h) supplies A[c1 = rt*32 + r][sample s0 + h] =
+// w * xc and B[sample s0 + h][c2 = ct*32 + r] = xc).  The D x D output is split into 32 x 32
+// tiles over the 4 wavefronts.  Each chunk writes its own partial; k_gmm_cov_reduce sums the
+// chunks in a fixed order (deterministic, no float atomics).  blockIdx.x = k varies fastest, so
+// the K workgroups of one chunk run together and share its rows through L2 / MALL.
+constexpr int kCovRB = 64;
+
+struct CovArgs {
+    const float *x;
+    const float *resp;
+    const float *means;
+    float *out;  // [chunks][K][d][d] partials (or [K][d][d] when chunks == 1)
+    int64_t V;
+    int64_t rows_per_chunk;
+    int d;
+    int K;
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) k_gmm_cov_mfma(CovArgs a) {
+    constexpr int CT = D / 32;
+    constexpr int TPW = CT * CT / 4;  // 32x32 tiles per wavefront
+    constexpr int LD = D + 4;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    __shared__ __attribute__((aligned(16))) float xs[kCovRB * LD];
+    __shared__ float ws[kCovRB];
+    __shared__ float mus[D];
+    const int k = blockIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    if (tid < D) mus[tid] = a.means[k * D + tid];
+    f32x16 acc[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+    for (int64_t b = c0; b < c1; b += kCovRB) {
+        __syncthreads();
+        for (int o = tid; o < kCovRB * D / 4; o += 256) {
+            const int s = (o * 4) / D, c = (o * 4) % D;
+            const int64_t row = b + s;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < c1) v = reinterpret_cast<const float4 *>(a.x + row * D)[c / 4];
+            float *dst = xs + s * LD + c;
+            dst[0] = v.x - mus[c];
+            dst[1] = v.y - mus[c + 1];
+            dst[2] = v.z - mus[c + 2];
+            dst[3] = v.w - mus[c + 3];
+        }
+        if (tid < kCovRB) ws[tid] = b + tid < c1 ? a.resp[(b + tid) * a.K + k] : 0.0f;
+        __syncthreads();
+#pragma unroll 4
+        for (int s0 = 0; s0 < kCovRB; s0 += 2) {
+            const float *row = xs + (s0 + h) * LD;
+            const float w = ws[s0 + h];
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const int tile = wid * TPW + t;
+                const int rt = tile / CT, ct = tile % CT;
+                const float av = w * row[rt * 32 + r];
+                const float bv = row[ct * 32 + r];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+            }
+        }
+    }
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * D * D;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int tile = wid * TPW + t;
+        const int rt = tile / CT, ct = tile % CT;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            out[i * D + ct * 32 + r] = acc[t][e];
+        }
+    }
+}
+
+// Any d <= 128 on the VALU: thread owns entries tid + 256 q of the d x d output.
+__global__ void __launch_bounds__(256) k_gmm_cov_valu(CovArgs a) {
+    constexpr int MAXQ = 64;  // 128 * 128 / 256
+    __shared__ float xs[kCovRB * 129];
+    __shared__ float ws[kCovRB];
+    const int d = a.d, k = blockIdx.x, tid = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int ne = d * d;
+    float acc[MAXQ];
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) acc[q] = 0.0f;
+    for (int64_t b = c0; b < c1; b += kCovRB) {
+        __syncthreads();
+        for (int o = tid; o < kCovRB * d; o += 256) {
+            const int s = o / d, c = o % d;
+            xs[s * 129 + c] = b + s < c1 ? a.x[(b + s) * d + c] - a.means[k * d + c] : 0.0f;
+        }
+        if (tid < kCovRB) ws[tid] = b + tid < c1 ? a.resp[(b + tid) * a.K + k] : 0.0f;
+        __syncthreads();
+        const int nb = (int)((c1 - b) < kCovRB ? (c1 - b) : kCovRB);
+        for (int s = 0; s < nb; ++s) {
+            const float w = ws[s];
+            const float *row = xs + s * 129;
+#pragma unroll
+            for (int q = 0; q < MAXQ; ++q) {
+                const int e = tid + 256 * q;
+                if (e < ne) acc[q] = __builtin_fmaf(w * row[e / d], row[e % d], acc[q]);
+            }
+        }
+    }
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * ne;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+        const int e = tid + 256 * q;
+        if (e < ne) out[e] = acc[q];
+    }
+}
+
+// out[i] = sum_c part[c][i] in chunk order (deterministic), i over K d^2 entries.
+__global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float *out, int64_t n,
+                                                        int chunks) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.0f;
+    for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * n + i];
+    out[i] = s;
 }
 
 }  // namespace come
@@ -346,6 +487,12 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
 extern "C" int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol,
                              const float *mu_prec, const float *log_norm, int K, float *resp_out,
                              void *stream) {
+    return come_gmm_estep(x, V, d, prec_chol, mu_prec, log_norm, K, resp_out, nullptr, stream);
+}
+
+extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol,
+                              const float *mu_prec, const float *log_norm, int K, float *resp_out,
+                              float *lse_out, void *stream) {
     if (V < 0 || d < 1 || d > 128 || K < 1 || K > 64)
         return set_error(COME_E_INVALID, "gmm_resp: need V>=0, 1<=d<=128, 1<=K<=64");
     if (V == 0) return COME_OK;
@@ -354,7 +501,7 @@ extern "C" int come_gmm_resp(const float *x, int64_t V, int d, const float *prec
     int dev;
     int rc = ensure_init(&dev);
     if (rc) return rc;
-    RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, V, d, K};
+    RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K};
     if ((d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0) {
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(d * d + d);
@@ -380,4 +527,32 @@ extern "C" int come_gmm_resp(const float *x, int64_t V, int d, const float *prec
     }
     hipLaunchKernelGGL(k_gmm_resp, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, a);
     return hip_error(hipGetLastError(), "k_gmm_resp launch");
+}
+
+extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *resp,
+                                const float *means, int K, int chunks, float *scratch,
+                                float *scatter_out, void *stream) {
+    if (V < 0 || d < 1 || d > 128 || K < 1 || chunks < 1 || chunks > 65535)
+        return set_error(COME_E_INVALID, "gmm_scatter: need V>=0, 1<=d<=128, K>=1, "
+                                         "1<=chunks<=65535");
+    if (!x || !resp || !means || !scatter_out || (chunks > 1 && !scratch))
+        return set_error(COME_E_INVALID, "null pointer");
+    int dev;
+    int rc = ensure_init(&dev);
+    if (rc) return rc;
+    const int64_t n = (int64_t)K * d * d;
+    int64_t per = (V + chunks - 1) / chunks;
+    per = (per + kCovRB - 1) / kCovRB * kCovRB;
+    if (per < kCovRB) per = kCovRB;
+    const int used = V == 0 ? 1 : (int)((V + per - 1) / per);
+    CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K};
+    const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
+    void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu
+                                  : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
+    hipLaunchKernelGGL(kern, dim3(K, used), dim3(256), 0, (hipStream_t)stream, a);
+    rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
+    if (rc || used == 1) return rc;
+    hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+    return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
 }

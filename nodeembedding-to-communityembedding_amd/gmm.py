@@ -1,0 +1,283 @@
+"""Full-covariance Gaussian mixture EM on the GPU -- replaces the reference's
+``sklearn.mixture.GaussianMixture(n_components=k, covariance_type='full', n_init=10,
+reg_covar=...).fit(X)`` (ADSCModel/community_embeddings.py:18,27).
+
+Same estimator surface as sklearn for the parts the reference uses: constructor arguments
+(n_components, covariance_type='full' only, tol, reg_covar, max_iter, n_init, init_params=
+'kmeans' | 'random', weights_init, means_init, precisions_init, random_state), ``fit``,
+``predict_proba``, ``predict``, ``score``, and the fitted attributes ``weights_``, ``means_``,
+``covariances_``, ``precisions_cholesky_``, ``precisions_``, ``converged_``, ``n_iter_``,
+``lower_bound_`` (numpy float64, as sklearn returns them).
+
+The EM loop follows sklearn's BaseMixture.fit_predict: for each init, E-step / M-step until the
+change of the mean log-likelihood is below ``tol`` (or ``max_iter``), keep the init with the best
+lower bound, and finish with one more E-step.  Per iteration the two 2 V K d^2 contractions run
+in libcome.so: the E-step (come_gmm_estep: MFMA X P_k, per-row logsumexp, responsibilities) and
+the M-step scatter matrices (come_gmm_scatter: MFMA sum_i r_ik (x_i - mu_k)(x_i - mu_k)^T).
+The K x d plain GEMM for the means (resp^T X) and the K small Cholesky factorisations (float64)
+run through torch on the same device.
+
+Parity: with fixed initial parameters the iterations match sklearn's within fp32 tolerance
+(tests/test_gpu_gmm.py).  The default k-means initialisation (k-means++ seeding then Lloyd,
+sklearn's KMeans(n_init=1) semantics) draws from its own device generator, so -- like the
+reference, whose GaussianMixture is unseeded -- which local optimum a fit reaches is not pinned.
+"""
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr, stream_handle
+
+
+def _as_device_x(X, device=None):
+    import torch
+    if isinstance(X, torch.Tensor):
+        t = X.detach()
+        if device is not None:
+            t = t.to(device)
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
+        t = t.to(device if device is not None else torch.device("cuda",
+                                                                 torch.cuda.current_device()))
+    if not t.is_cuda:
+        raise TypeError("GaussianMixture runs on the GPU: X must be (or move to) a CUDA tensor")
+    return t.to(torch.float32).contiguous()
+
+
+def estep(X, prec_chol, mu_prec, log_norm):
+    """(resp [V, K], lse [V]) for device fp32 X and precomputed component parameters."""
+    import torch
+    V, d = X.shape
+    K = prec_chol.shape[0]
+    resp = torch.empty((V, K), dtype=torch.float32, device=X.device)
+    lse = torch.empty((V,), dtype=torch.float32, device=X.device)
+    check(_lib.lib().come_gmm_estep(ptr(X), V, d, ptr(prec_chol), ptr(mu_prec), ptr(log_norm), K,
+                                    ptr(resp), ptr(lse), stream_handle(X.device)),
+          "come_gmm_estep")
+    return resp, lse
+
+
+def scatter(X, resp, means, chunks=None):
+    """[K, d, d] device fp32: sum_i resp[i,k] (x_i - means_k)(x_i - means_k)^T."""
+    import torch
+    V, d = X.shape
+    K = resp.shape[1]
+    if chunks is None:  # >= ~1024 workgroups, partials <= 256 MB
+        chunks = max(1, min(-(-1024 // K), (64 << 20) // max(1, K * d * d), -(-V // 64)))
+    out = torch.empty((K, d, d), dtype=torch.float32, device=X.device)
+    scratch = torch.empty((chunks * K * d * d,) if chunks > 1 else (1,), dtype=torch.float32,
+                          device=X.device)
+    means = means.to(torch.float32).contiguous()
+    resp = resp.contiguous()
+    check(_lib.lib().come_gmm_scatter(ptr(X), V, d, ptr(resp), ptr(means), K, int(chunks),
+                                      ptr(scratch), ptr(out), stream_handle(X.device)),
+          "come_gmm_scatter")
+    return out
+
+
+class GaussianMixture(object):
+    def __init__(self, n_components=1, covariance_type='full', tol=1e-3, reg_covar=1e-6,
+                 max_iter=100, n_init=1, init_params='kmeans', weights_init=None,
+                 means_init=None, precisions_init=None, random_state=None, kmeans_max_iter=300,
+                 kmeans_tol=1e-4, device=None):
+        if covariance_type != 'full':
+            raise NotImplementedError("only covariance_type='full' (the reference's) is "
+                                      "implemented")
+        if init_params not in ('kmeans', 'random'):
+            raise ValueError("init_params must be 'kmeans' or 'random'")
+        self.n_components = int(n_components)
+        self.covariance_type = covariance_type
+        self.tol = float(tol)
+        self.reg_covar = float(reg_covar)
+        self.max_iter = int(max_iter)
+        self.n_init = int(n_init)
+        self.init_params = init_params
+        self.weights_init = weights_init
+        self.means_init = means_init
+        self.precisions_init = precisions_init
+        self.random_state = random_state
+        self.kmeans_max_iter = int(kmeans_max_iter)
+        self.kmeans_tol = float(kmeans_tol)
+        self.device = device
+
+    # ---- parameters -------------------------------------------------------------------------
+    def _m_step(self, X, resp):
+        """sklearn _estimate_gaussian_parameters (full): nk, means, covariances (+ reg)."""
+        import torch
+        V, d = X.shape
+        nk = resp.sum(0, dtype=torch.float64) + 10 * np.finfo(np.float64).eps
+        means = (resp.t() @ X).double() / nk[:, None]
+        S = scatter(X, resp, means.float())
+        cov = S.double() / nk[:, None, None]
+        cov += self.reg_covar * torch.eye(d, dtype=torch.float64, device=X.device)
+        return nk / V, means, cov
+
+    def _set_params(self, weights, means, cov):
+        import torch
+        d = means.shape[1]
+        chol, info = torch.linalg.cholesky_ex(cov)
+        if bool((info != 0).any()):
+            raise ValueError("Fitting the mixture model failed because some components have "
+                             "ill-defined empirical covariance (for instance caused by "
+                             "singleton or collapsed samples). Try to decrease the number of "
+                             "components, or increase reg_covar.")
+        eye = torch.eye(d, dtype=torch.float64, device=cov.device).expand_as(cov)
+        prec_chol = torch.linalg.solve_triangular(chol, eye, upper=False).transpose(-1, -2)
+        self._w, self._mu, self._cov, self._pc = weights, means, cov, prec_chol.contiguous()
+        self._prepare_estep()
+
+    def _set_params_from_precisions(self, weights, means, precisions):
+        import torch
+        pchol = torch.linalg.cholesky(precisions)  # sklearn: cholesky of the precision, lower
+        self._w, self._mu, self._pc = weights, means, pchol.contiguous()
+        self._cov = torch.cholesky_inverse(pchol)
+        self._prepare_estep()
+
+    def _prepare_estep(self):
+        import torch
+        d = self._mu.shape[1]
+        log_det = torch.log(torch.diagonal(self._pc, dim1=-2, dim2=-1)).sum(-1)
+        self._e_pc = self._pc.float().contiguous()
+        self._e_mp = torch.einsum("kd,kde->ke", self._mu, self._pc).float().contiguous()
+        self._e_ln = (torch.log(self._w) + log_det - 0.5 * d * math.log(2 * math.pi)).float() \
+            .contiguous()
+
+    # ---- initialisation ------------------------------------------------------------------------
+    def _generator(self, device):
+        import torch
+        g = torch.Generator(device=device)
+        rs = self.random_state
+        if rs is None:
+            seed = int(np.random.randint(0, 2 ** 31 - 1))  # like sklearn: the global RNG
+        elif isinstance(rs, (int, np.integer)):
+            seed = int(rs)
+        else:
+            seed = int(rs.randint(0, 2 ** 31 - 1))
+        g.manual_seed(seed)
+        return g
+
+    def _kmeans_labels(self, X, gen):
+        """KMeans(n_clusters=K, n_init=1): greedy k-means++ seeding (2 + log K local trials,
+        sklearn's _kmeans_plusplus) then Lloyd iterations until the squared centre shift is
+        <= tol * mean feature variance."""
+        import torch
+        V, d = X.shape
+        K = self.n_components
+        xx = (X * X).sum(1)
+        trials = 2 + int(math.log(K))
+        first = torch.randint(0, V, (1,), generator=gen, device=X.device)
+        centers = [X[first[0]]]
+        closest = (xx - 2 * X @ centers[0] + centers[0].dot(centers[0])).clamp_min(0)
+        pot = closest.sum()
+        for _ in range(1, K):
+            r = torch.rand(trials, generator=gen, device=X.device, dtype=torch.float64) * pot
+            cand = torch.searchsorted(torch.cumsum(closest.double(), 0), r).clamp_max(V - 1)
+            C = X[cand]
+            dist = (xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]).clamp_min(0)
+            dist = torch.minimum(dist, closest[:, None])
+            pots = dist.sum(0)
+            best = int(torch.argmin(pots))
+            closest, pot = dist[:, best].contiguous(), pots[best]
+            centers.append(C[best])
+        C = torch.stack(centers)
+        tol = self.kmeans_tol * float(X.var(0).mean())
+        labels = None
+        for _ in range(self.kmeans_max_iter):
+            dist = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]
+            labels = torch.argmin(dist, 1)
+            cnt = torch.bincount(labels, minlength=K).float()
+            S = torch.zeros((K, d), dtype=torch.float32, device=X.device)
+            S.index_add_(0, labels, X)
+            newC = torch.where(cnt[:, None] > 0, S / cnt.clamp_min(1)[:, None], C)
+            shift = float(((newC - C) ** 2).sum())
+            C = newC
+            if shift <= tol:
+                break
+        dist = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]
+        return torch.argmin(dist, 1)
+
+    def _initialize(self, X, gen):
+        import torch
+        V, d = X.shape
+        K = self.n_components
+        if self.init_params == 'kmeans':
+            labels = self._kmeans_labels(X, gen)
+            resp = torch.zeros((V, K), dtype=torch.float32, device=X.device)
+            resp[torch.arange(V, device=X.device), labels] = 1.0
+        else:
+            resp = torch.rand((V, K), generator=gen, device=X.device)
+            resp /= resp.sum(1, keepdim=True)
+        w, mu, cov = self._m_step(X, resp)
+        dev = X.device
+        if self.weights_init is not None:
+            w = torch.as_tensor(np.asarray(self.weights_init, np.float64), device=dev)
+        if self.means_init is not None:
+            mu = torch.as_tensor(np.asarray(self.means_init, np.float64), device=dev)
+        if self.precisions_init is not None:
+            P = torch.as_tensor(np.asarray(self.precisions_init, np.float64), device=dev)
+            self._set_params_from_precisions(w, mu, P)
+        else:
+            self._set_params(w, mu, cov)
+
+    # ---- EM ------------------------------------------------------------------------------------
+    def fit(self, X, y=None):
+        self.fit_predict(X)
+        return self
+
+    def fit_predict(self, X, y=None):
+        import torch
+        X = _as_device_x(X, self.device)
+        V, d = X.shape
+        if V < self.n_components:
+            raise ValueError("Expected n_samples >= n_components but got n_components = %d, "
+                             "n_samples = %d" % (self.n_components, V))
+        if self.n_components > 64 or d > 128:
+            raise ValueError("GPU GaussianMixture supports n_components <= 64 and d <= 128")
+        gen = self._generator(X.device)
+        best, max_lb = None, -np.inf
+        self.converged_ = False
+        for _ in range(self.n_init):
+            self._initialize(X, gen)
+            lb = -np.inf
+            converged, n_iter = False, 0
+            for n_iter in range(1, self.max_iter + 1):
+                prev = lb
+                resp, lse = estep(X, self._e_pc, self._e_mp, self._e_ln)
+                w, mu, cov = self._m_step(X, resp)
+                self._set_params(w, mu, cov)
+                lb = float(lse.double().mean())
+                if abs(lb - prev) < self.tol:
+                    converged = True
+                    break
+            if lb > max_lb or max_lb == -np.inf:
+                max_lb = lb
+                best = (self._w, self._mu, self._cov, self._pc, n_iter, converged)
+        self._w, self._mu, self._cov, self._pc, self.n_iter_, self.converged_ = best
+        self._prepare_estep()
+        self.lower_bound_ = max_lb
+        resp, _ = estep(X, self._e_pc, self._e_mp, self._e_ln)
+        self._export()
+        return torch.argmax(resp, 1)
+
+    def _export(self):
+        import torch
+        self.weights_ = self._w.cpu().numpy()
+        self.means_ = self._mu.cpu().numpy()
+        self.covariances_ = self._cov.cpu().numpy()
+        self.precisions_cholesky_ = self._pc.cpu().numpy()
+        pc = self._pc
+        self.precisions_ = torch.matmul(pc, pc.transpose(-1, -2)).cpu().numpy()
+
+    # ---- inference ----------------------------------------------------------------------------
+    def predict_proba(self, X):
+        X = _as_device_x(X, self.device)
+        return estep(X, self._e_pc, self._e_mp, self._e_ln)[0]
+
+    def predict(self, X):
+        import torch
+        return torch.argmax(self.predict_proba(X), 1)
+
+    def score(self, X, y=None):
+        X = _as_device_x(X, self.device)
+        return float(estep(X, self._e_pc, self._e_mp, self._e_ln)[1].double().mean())
