@@ -126,6 +126,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: blocking delta all-reduce instead of overlapping it with the next "
+                         "batch")
+    ap.add_argument("--plain-table", action="store_true",
+                    help="draw negatives from the 400 MB uint32 table instead of its packed form")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
@@ -176,17 +181,29 @@ def main():
     pairs_per_step = [int(o2_pairs_of_lengths(lengths[s * B:(s + 1) * B], w))
                       for s in range(total_steps)]
     sync = DeltaAllReduce([model.node_embedding, model.context_embedding]) if world > 1 else None
+    # the exact packed negative table (come_pack_table) unless --plain-table
+    neg_table = model.table if args.plain_table else model.negative_table()
 
     def step(s):
         tsi.sgns_o2(model.node_embedding, model.context_embedding, walks_all[s * B:(s + 1) * B],
-                    seeds_all[s * B:(s + 1) * B], w, n, model.table, args.lr, 1.0,
+                    seeds_all[s * B:(s + 1) * B], w, n, neg_table, args.lr, 1.0,
                     tsi.MODE_HOGWILD)
 
     stream = torch.cuda.current_stream(dev)
+    def exchange():
+        # overlapped: start() finishes the previous exchange (device-side wait + apply), then
+        # launches this batch's all-reduce on RCCL's stream, which runs beside the next batch
+        if args.no_overlap:
+            sync.sync()
+        else:
+            sync.start()
+
     for s in range(args.warmup):
         step(s)
         if sync is not None and (s + 1) % args.sync_every == 0:
-            sync.sync()
+            exchange()
+    if sync is not None:
+        sync.finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -201,7 +218,9 @@ def main():
         step(s)
         ev[k][1].record(stream)
         if sync is not None and (k + 1) % args.sync_every == 0:
-            sync.sync()
+            exchange()
+    if sync is not None:
+        sync.finish()  # the last exchange is inside the timed region, not overlapped
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -285,8 +304,9 @@ def main():
             "walks_per_step_per_gpu": B,
             "pairs_per_step_per_gpu": pairs_rank_step,
             "sync_every_steps": args.sync_every if world > 1 else None,
-            "parallelism": "walk-shard dp%d + delta all-reduce (%s)" % (
-                world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend)
+            "parallelism": "walk-shard dp%d + %s delta all-reduce (%s)" % (
+                world, "blocking" if args.no_overlap else "overlapped",
+                "RCCL" if args.dist_backend == "nccl" else args.dist_backend)
             if world > 1 else "single GPU, Hogwild over walks",
         },
         "roofline": {

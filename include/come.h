@@ -45,6 +45,10 @@ enum {
                                  anchor, bit-exact with oracle/ in its WAVE64 dot order */
 };
 
+/* Flag OR-ed into `mode` of come_sgns_o2 / come_sgns_o1: `table` points to come_pack_table's
+ * packed words (T still the logical number of slots) instead of the uint32 table. */
+#define COME_TABLE_PACKED 0x100
+
 int come_abi_version(void);
 const char *come_last_error(void);
 
@@ -73,6 +77,16 @@ int come_fast_version(void);
 int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,
                  int L, const uint64_t *seeds, int window, int negative, const uint32_t *table,
                  uint64_t T, float lr, float alpha, int mode, void *stream);
+
+/* ---- Packed negative table: an exact, 16x smaller equivalent of make_table's output ----
+ * packed: device, 16 * ceil(T / 64) bytes, 16-byte aligned; word w = {uint32 base = table[64w],
+ * uint32 0, uint64 bits} with bit i (1..63) set iff table[64w+i] == table[64w+i-1] + 1, so
+ * table[64w+i] = base + popcount(bits & (2^(i+1) - 1)).  Exact when every step inside a word is
+ * 0 or 1, which make_table guarantees (model.py:107-121 advances at most one id per slot).
+ * status: device int32, set to 0 if the table packed exactly, 1 if some step was not 0/1 (then
+ * the packed words must not be used).  Asynchronous on `stream`. */
+int come_pack_table(const uint32_t *table, uint64_t T, void *packed, int32_t *status,
+                    void *stream);
 
 /* ---- SGNS, first order (edges): replaces train_o1 (pyx:407-450) over a batch ----
  * edges       device int32 [E x 2] rows (u, v): pair (input u, positive v) then (input v,
@@ -172,6 +186,16 @@ int come_write_int_rows(const char *path, const int64_t *rows, int64_t nrows, in
 int come_save_embedding(const char *path, const float *emb, int64_t V, int d, int64_t first_id);
 /* str(np.float32(x)) into out32 (NUL-terminated); returns its length. */
 int come_format_f32(float x, char *out32);
+
+/* ---- Multi-GPU delta exchange (come_amd.distributed.DeltaAllReduce, overlapped) ----
+ * Fused elementwise passes around the all-reduce of a replicated table of n floats (device,
+ * 16-byte aligned, n % 4 == 0):
+ *   come_delta_begin:  D = W - S;  Down = D           (D is then all-reduced in place)
+ *   come_delta_end:    S += Dsum;  W += Dsum - Down   (Dsum = the all-reduced D) */
+int come_delta_begin(const float *W, const float *S, float *D, float *Down, int64_t n,
+                     void *stream);
+int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int64_t n,
+                   void *stream);
 
 /* ---- Tuning ----
  * Process-wide launch knobs for experiments (0 = automatic): "o2_kernel" (1 direct, 2 ring),

@@ -11,6 +11,7 @@ LIB_PATH = os.path.join(HERE, "libcome.so")
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
+TABLE_PACKED = 0x100  # COME_TABLE_PACKED mode flag
 
 # Every symbol include/come.h declares (checked by tests/test_capi.py).
 SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
@@ -19,7 +20,8 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_random_walks", "come_walks_reference", "come_pyrandom_seed",
            "come_pyrandom_draw", "come_graph_from_edges", "come_read_int_rows",
            "come_write_int_rows", "come_save_embedding", "come_format_f32",
-           "come_gmm_estep", "come_gmm_scatter")
+           "come_gmm_estep", "come_gmm_scatter", "come_pack_table",
+           "come_delta_begin", "come_delta_end")
 
 _lib = None
 
@@ -54,6 +56,9 @@ def lib():
     L.come_sgns_o1.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, P]
     L.come_community_grad.argtypes = [P, i64, i32, P, P, P, i32, f32, f32, i32, P]
     L.come_gmm_resp.argtypes = [P, i64, i32, P, P, P, i32, P, P]
+    L.come_pack_table.argtypes = [P, u64, P, P, P]
+    L.come_delta_begin.argtypes = [P, P, P, P, i64, P]
+    L.come_delta_end.argtypes = [P, P, P, P, i64, P]
     L.come_gmm_estep.argtypes = [P, i64, i32, P, P, P, i32, P, P, P]
     L.come_gmm_scatter.argtypes = [P, i64, i32, P, P, i32, i32, P, P, P]
     L.come_make_table.argtypes = [P, i64, P, u64, f64]

@@ -53,7 +53,7 @@ class Context2Vec(object):
             w = torch.from_numpy(np.ascontiguousarray(rows[s:s + self.batch_walks])).to(dev)
             sd = torch.from_numpy(seeds[s:s + self.batch_walks].view(np.int64)).to(dev)
             tsi.sgns_o2(model.node_embedding, model.context_embedding, w, sd, self.window_size,
-                        self.negative, model.table, self.lr, alpha, mode)
+                        self.negative, model.negative_table(), self.lr, alpha, mode)
         torch.cuda.synchronize(dev)
         elapsed = time.time() - start
         nodes = int((rows >= 0).sum()) + node_count

@@ -55,7 +55,11 @@ static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int bl
 using namespace come;
 
 static int check_common(int64_t V, int d, int negative, const uint32_t *table, uint64_t T,
-                        int mode) {
+                        int &mode, int &packed) {
+    packed = (mode & COME_TABLE_PACKED) ? 1 : 0;
+    mode &= ~COME_TABLE_PACKED;
+    if (packed && ((uintptr_t)table % 16) != 0)
+        return set_error(COME_E_INVALID, "packed table must be 16-byte aligned");
     if (V <= 0) return set_error(COME_E_INVALID, "V must be > 0 (got %lld)", (long long)V);
     if (V > INT32_MAX)
         return set_error(COME_E_INVALID, "V must fit int32 row indices (got %lld)", (long long)V);
@@ -82,7 +86,8 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
                             int64_t P, int L, const uint64_t *seeds, int window, int negative,
                             const uint32_t *table, uint64_t T, float lr, float alpha, int mode,
                             void *stream) {
-    int rc = check_common(V, d, negative, table, T, mode);
+    int packed = 0;
+    int rc = check_common(V, d, negative, table, T, mode, packed);
     if (rc) return rc;
     if (P < 0 || L < 0 || window < 0)
         return set_error(COME_E_INVALID, "P, L and window must be >= 0");
@@ -92,7 +97,7 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
     if (!aligned_for(node, d) || !aligned_for(ctx, d))
         return set_error(COME_E_INVALID, "node/ctx must be 16-byte aligned for d=%d", d);
     O2Args a{node, ctx, walks, seeds, table, V, P, L, d, window, negative, lr, alpha,
-             make_fastmod(T)};
+             make_fastmod(T), packed};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
     const int mi = maxn_index(negative);
@@ -120,7 +125,8 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
 extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
                             const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
                             float lr, int mode, void *stream) {
-    int rc = check_common(V, d, negative, table, T, mode);
+    int packed = 0;
+    int rc = check_common(V, d, negative, table, T, mode, packed);
     if (rc) return rc;
     if (E < 0) return set_error(COME_E_INVALID, "E must be >= 0");
     if (E == 0) return COME_OK;
@@ -129,10 +135,54 @@ extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges,
         return set_error(COME_E_INVALID, "O1 supports negative <= 32 (got %d)", negative);
     if (!aligned_for(node, d))
         return set_error(COME_E_INVALID, "node must be 16-byte aligned for d=%d", d);
-    O1Args a{node, edges, seeds, table, V, E, d, negative, lr, make_fastmod(T)};
+    O1Args a{node, edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
     return launch(ks.o1[full][maxn_index(negative)], &a, E, mode, 4, 8, 0, stream);
+}
+
+// One wavefront per 64-slot word: lane i loads slot 64w + i (one coalesced 256-B read), the
+// steps to the previous lane are balloted into the word's bit mask; a step other than 0 or 1
+// marks the table unpackable (status = 1).
+__global__ void __launch_bounds__(256) k_pack_table(const uint32_t *__restrict__ table, uint64_t T,
+                                                    uint4 *__restrict__ packed,
+                                                    int32_t *__restrict__ status) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t words = (T + 63) / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    bool bad = false;
+    for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < words;
+         w += nwaves) {
+        const uint64_t s = w * 64 + lane;
+        const uint32_t v = s < T ? table[s] : 0u;
+        const uint32_t prev = (uint32_t)__shfl_up((int)v, 1);
+        const uint32_t step = v - prev;
+        const bool inc = lane > 0 && s < T && step == 1u;
+        bad |= lane > 0 && s < T && step > 1u;
+        const uint64_t bits = __ballot(inc);
+        if (lane == 0) packed[w] = make_uint4(v, 0u, (uint32_t)bits, (uint32_t)(bits >> 32));
+    }
+    if (__any(bad) && lane == 0) atomicOr(status, 1);
+}
+
+extern "C" int come_pack_table(const uint32_t *table, uint64_t T, void *packed, int32_t *status,
+                               void *stream) {
+    if (!table || !packed || !status || T == 0)
+        return set_error(COME_E_INVALID, "pack_table: null pointer or empty table");
+    if (((uintptr_t)packed % 16) != 0)
+        return set_error(COME_E_INVALID, "packed table must be 16-byte aligned");
+    int dev = 0;
+    int rc = ensure_init(&dev);
+    if (rc) return rc;
+    hipError_t e = hipMemsetAsync(status, 0, sizeof(int32_t), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_error(e, "hipMemsetAsync(status)");
+    const uint64_t words = (T + 63) / 64;
+    uint64_t blocks = (words + 3) / 4;
+    const uint64_t cap = (uint64_t)num_cus(dev) * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_pack_table, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       table, T, (uint4 *)packed, status);
+    return hip_error(hipGetLastError(), "k_pack_table launch");
 }
 
 extern "C" int come_upload_exp_table(const float *host1000) {

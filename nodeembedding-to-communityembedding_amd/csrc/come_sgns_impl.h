@@ -55,6 +55,29 @@ __device__ inline uint32_t table_slot(uint64_t s, uint64_t m, uint32_t d) {
     return (uint32_t)__umul64hi(m * (uint64_t)x, (uint64_t)d);
 }
 
+// Packed negative table (come_pack_table): word w = {base, unused, bits} covers slots
+// [64w, 64w + 64); table[64w + i] = base + popcount(bits & ((2 << i) - 1)), bit i (i >= 1) set iff
+// slot i holds one more than slot i - 1.  Exact for every table whose values step by 0 or 1
+// inside each 64-slot word -- make_table's are (model.py:107-121 advances widx by at most one per
+// slot).  One 16-B load per draw from a T/4-byte structure (25 MB at T = 1e8, Infinity-Cache
+// resident) instead of a 4-B load from the 400 MB table.
+struct PackedWord {
+    uint32_t base;
+    uint32_t unused;
+    uint64_t bits;
+};
+
+template <class Args>
+__device__ inline uint32_t table_value(const Args &a, uint32_t slot) {
+    if (a.packed) {
+        const uint4 w = reinterpret_cast<const uint4 *>(a.table)[slot >> 6];
+        const uint64_t bits = ((uint64_t)w.w << 32) | w.z;
+        const uint64_t mask = (2ull << (slot & 63)) - 1ull;  // slot & 63 == 63: all ones
+        return w.x + (uint32_t)__popcll(bits & mask);
+    }
+    return a.table[slot];
+}
+
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float uniformf(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -150,14 +173,13 @@ struct DrawBatch {
     int used;         // draws of the batch already consumed (wave-uniform)
 };
 
+template <class Args>
 __device__ inline void draws_fill(DrawBatch &b, uint64_t state0, const LcgLane &lc,
-                                  const uint32_t *__restrict__ table, FastMod fm, int64_t V) {
+                                  const Args &a) {
     b.base = state0;
     b.used = 0;
     const uint64_t s = (lc.a * state0 + lc.c) & kLcgMask;
-    const uint32_t slot = table_slot(s, fm.m, fm.d);
-    uint32_t t = table[slot];
-    b.target = t;
+    b.target = table_value(a, table_slot(s, a.fm.m, a.fm.d));
 }
 
 // State of the draw `b.used` positions after the batch base (0 < used <= 64).
@@ -178,7 +200,7 @@ struct DrawPipe {
     template <class Args>
     __device__ inline uint32_t gather(uint64_t base, const LcgLane &lc, const Args &a) {
         const uint64_t s = (lc.a * base + lc.c) & kLcgMask;  // draw base + lane
-        return a.table[table_slot(s, a.fm.m, a.fm.d)];
+        return table_value(a, table_slot(s, a.fm.m, a.fm.d));
     }
 };
 
@@ -199,6 +221,7 @@ struct O2Args {
     float lr;
     float alpha;
     FastMod fm;
+    int packed;  // table points to come_pack_table's words
 };
 
 // State 64 draws after `base` (lane 63's state advanced once).
@@ -218,7 +241,7 @@ __device__ inline void o2_pair(const O2Args &a, DrawBatch &db, const LcgLane &lc
     using R = Row<VEC, FULL>;
     const int n = a.negative;
     const int d = a.d;
-    if (n > 0 && db.used + n > 64) draws_fill(db, draws_state_at_used(db, lc), lc, a.table, a.fm, a.V);
+    if (n > 0 && db.used + n > 64) draws_fill(db, draws_state_at_used(db, lc), lc, a);
     int t[MAXN + 1];
     bool valid[MAXN + 1];
     t[0] = ci;
@@ -333,7 +356,7 @@ __global__ void __launch_bounds__(256) k_sgns_o2(O2Args a) {
         db.used = 0;
         db.base = uniform64(a.seeds[p]);
         db.target = 0;
-        if (a.negative > 0) draws_fill(db, db.base, lc, a.table, a.fm, a.V);
+        if (a.negative > 0) draws_fill(db, db.base, lc, a);
         for (int i = 0; i < path_len; ++i) {
             const int ci = uniform(idx[i]);
             if (ci < 0 || ci >= a.V) continue;  // codelens[i] == 0 (pyx:495)
@@ -659,6 +682,7 @@ struct O1Args {
     int negative;
     float lr;
     FastMod fm;
+    int packed;
 };
 
 template <int VEC, bool FULL, int MAXN>
@@ -681,7 +705,7 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
         db.used = 0;
         db.base = uniform64(a.seeds[e]);
         db.target = 0;
-        if (n > 0) draws_fill(db, db.base, lc, a.table, a.fm, a.V);
+        if (n > 0) draws_fill(db, db.base, lc, a);
 
         int t1[MAXN + 1], t2[MAXN + 1];
         bool v1[MAXN + 1], v2[MAXN + 1];

@@ -14,6 +14,18 @@ changed:
 Summing deltas keeps every rank's Hogwild progress (plain averaging would shrink each rank's
 steps by 1/N).  With N = 1 sync is a no-op.  The all-reduce runs on torch.distributed with the
 "nccl" backend (= RCCL on ROCm); tests run the same code on "gloo" with CPU tensors.
+
+Overlap (``start`` / ``finish``): the exchange of batch s runs on RCCL's stream while batch s+1
+trains.  ``start`` snapshots the local delta D_r = W_r - W_sync and launches the asynchronous
+all-reduce of D; ``finish`` waits for it and applies the other ranks' deltas on top of whatever the
+rank trained meanwhile:
+
+    W      += sum_r D_r - D_own      (others' progress; own progress is already in W)
+    W_sync += sum_r D_r
+
+after which W - W_sync is exactly the rank's progress since ``start`` -- no update is lost or
+counted twice, and the replicas differ only by what each trained after ``start`` (Hogwild-style
+staleness of one batch).  ``sync`` = ``start`` + ``finish`` (no overlap).
 """
 import numpy as np
 
@@ -31,32 +43,87 @@ def shard_walks(walks, seeds, rank, world):
     return walks[lo:hi], seeds[lo:hi]
 
 
+def _fused(t):
+    """CUDA fp32 tables with n % 4 == 0 use the fused HIP passes (come_delta_begin/end); CPU
+    tensors (gloo tests) use the same arithmetic in torch ops."""
+    import torch
+    return t.is_cuda and t.dtype == torch.float32 and t.numel() % 4 == 0
+
+
+def _native(name, a, b, c, d):
+    from . import _lib
+    from ._lib import check, ptr, stream_handle
+    check(getattr(_lib.lib(), name)(ptr(a), ptr(b), ptr(c), ptr(d), a.numel(),
+                                    stream_handle(a.device)), name)
+
+
 class DeltaAllReduce(object):
     """Delta-sum synchronisation of a list of replicated tables (torch tensors, same shape on
     every rank).  ``bucket_elems`` bounds the size of each all-reduce call (large fp32 buckets:
     xGMI collectives are bandwidth-bound per link, so few big calls beat many small ones)."""
 
     def __init__(self, tables, group=None, bucket_elems=1 << 26):
+        import torch
         import torch.distributed as dist
         self.tables = list(tables)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket = int(bucket_elems)
         self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
+        self.dsum = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
+        self.down = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
+        self.pending = []
 
-    def sync(self):
+    def start(self):
+        """Snapshot this rank's delta and launch its asynchronous all-reduce (finishes any
+        exchange still pending first)."""
         if self.world == 1:
             return
         import torch.distributed as dist
+        self.finish()
+        for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
+            if _fused(t):
+                _native("come_delta_begin", t, s, ds, do)  # D = Down = W - W_sync
+            else:
+                ds.copy_(t)
+                ds.sub_(s)                                 # D_own = W - W_sync
+                do.copy_(ds)
+            flat = ds.view(-1)
+            for lo in range(0, flat.numel(), self.bucket):
+                hi = min(lo + self.bucket, flat.numel())
+                self.pending.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True))
+
+    def finish(self):
+        """Wait for the pending all-reduce (device-side wait on the current stream) and apply
+        the other ranks' deltas."""
+        if self.world == 1 or not self.pending:
+            return
+        for w in self.pending:
+            w.wait()
+        self.pending = []
+        for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
+            if _fused(t):
+                _native("come_delta_end", t, s, ds, do)    # S += Dsum; W += Dsum - Down
+            else:
+                s.add_(ds)                                 # W_sync += sum_r D_r
+                ds.sub_(do)                                # others' deltas
+                t.add_(ds)                                 # W += sum_r D_r - D_own
+
+    def sync(self):
+        """Blocking exchange: afterwards every replica equals W_sync + sum_r D_r, bit for bit
+        (nothing trained in between, so W is set to the new W_sync itself rather than to
+        W + others' deltas, which differs from it by rounding)."""
+        if self.world == 1:
+            return
+        self.start()
+        self.finish()
         for t, s in zip(self.tables, self.snap):
-            flat_t, flat_s = t.view(-1), s.view(-1)
-            for lo in range(0, flat_t.numel(), self.bucket):
-                hi = min(lo + self.bucket, flat_t.numel())
-                d = flat_t[lo:hi]
-                d.sub_(flat_s[lo:hi])                       # delta_r, in place
-                dist.all_reduce(d, op=dist.ReduceOp.SUM, group=self.group)
-                d.add_(flat_s[lo:hi])                       # W_sync + sum_r delta_r
-                flat_s[lo:hi].copy_(d)                      # new W_sync
+            t.copy_(s)
+
+    @property
+    def busy(self):
+        return bool(self.pending)
 
     def bytes_per_sync(self):
         return sum(t.numel() * t.element_size() for t in self.tables)

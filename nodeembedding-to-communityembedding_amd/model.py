@@ -10,7 +10,8 @@ Differences, all deliberate:
     (fp32 / uint32-as-int32); ``table_host`` keeps the numpy uint32 table;
   * ``make_table`` runs the exact native builder (come_make_table: same double accumulation,
     same start at node id 1 and the same clamp as model.py:107-121, O(V + T) instead of a Python
-    loop over T slots);
+    loop over T slots) and packs it on the device (``table_packed``, come_pack_table: the same
+    draws from a 16x smaller structure);
   * ``k`` may be given directly (no label file needed), ``device`` selects the GPU;
   * ``save``/``load_model`` use torch.save / torch.load(weights_only=True) (the reference's
     pickle-based load_model, model.py:133-140, is broken and unsafe);
@@ -135,6 +136,15 @@ class Model(object):
                                              self.table_size, float(power)), "come_make_table")
         self.table_host = table
         self.table = torch.from_numpy(table.view(np.int32)).to(self._torch_device())
+        self.table_packed = None
+        if self.table.is_cuda:
+            from .training_sdg_inner import pack_table
+            self.table_packed = pack_table(self.table)
+
+    def negative_table(self):
+        """What the trainers pass to the kernels: the exact packed form when it exists."""
+        return self.table_packed if getattr(self, "table_packed", None) is not None \
+            else self.table
 
     # ---- persistence ----
     def save(self, path='data', file_name=None):
@@ -145,7 +155,7 @@ class Model(object):
         os.makedirs(path, exist_ok=True)
         state = {}
         for k, v in self.__dict__.items():
-            if k == "_vocab":
+            if k in ("_vocab", "table_packed"):
                 continue
             if isinstance(v, np.ndarray):
                 state["np:" + k] = torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32
@@ -178,6 +188,10 @@ class Model(object):
         for k in ("node_embedding", "context_embedding", "centroid", "covariance_mat",
                   "inv_covariance_mat", "pi", "table"):
             setattr(m, k, getattr(m, k).to(dev))
+        m.table_packed = None
+        if m.table.is_cuda:
+            from .training_sdg_inner import pack_table
+            m.table_packed = pack_table(m.table)
         log.info('model loaded, size: %d table_size: %d down_sampling: %.5f communities %d' %
                  (m.layer1_size, m.table_size, m.down_sampling, m.k))
         return m

@@ -52,7 +52,8 @@ class Node2Vec(object):
         for _ in range(int(iter)):
             seeds = tsi.draw_seeds(rows.shape[0])
             sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
-            tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.table, self.lr, mode)
+            tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.negative_table(),
+                        self.lr, mode)
         torch.cuda.synchronize(dev)
         pairs = 2 * int((rows >= 0).all(axis=1).sum()) * int(iter)
         elapsed = time.time() - start

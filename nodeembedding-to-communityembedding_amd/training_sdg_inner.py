@@ -21,7 +21,7 @@ of one Python call per walk.
 import numpy as np
 
 from . import _lib
-from ._lib import MODE_HOGWILD, MODE_SEQUENTIAL, check, ptr, stream_handle
+from ._lib import MODE_HOGWILD, MODE_SEQUENTIAL, TABLE_PACKED, check, ptr, stream_handle
 
 FAST_VERSION = 0
 MAX_SENTENCE_LEN = 10000
@@ -60,18 +60,49 @@ def _require_cuda(t, name, dtype):
         raise ValueError("%s must be contiguous" % name)
 
 
+class PackedTable(object):
+    """Exact 16x smaller device form of a negative table (come_pack_table): ``words`` is a CUDA
+    int32 tensor [ceil(T/64), 4], ``T`` the number of slots.  Accepted wherever a table is."""
+
+    def __init__(self, words, T):
+        self.words, self.T = words, int(T)
+
+
+def pack_table(table):
+    """Pack a CUDA uint32-as-int32 table [T]; returns a PackedTable, or None if some step inside
+    a 64-slot word is not 0 or 1 (then keep using the plain table)."""
+    import torch
+    _require_cuda(table, "table", torch.int32)
+    T = table.numel()
+    words = torch.empty(((T + 63) // 64, 4), dtype=torch.int32, device=table.device)
+    status = torch.empty(1, dtype=torch.int32, device=table.device)
+    check(_lib.lib().come_pack_table(ptr(table), T, ptr(words), ptr(status),
+                                     stream_handle(table.device)), "come_pack_table")
+    return PackedTable(words, T) if int(status.item()) == 0 else None
+
+
+def _table_args(table):
+    """(pointer, T, mode flag) for a plain CUDA table tensor or a PackedTable."""
+    import torch
+    if isinstance(table, PackedTable):
+        return ptr(table.words), table.T, TABLE_PACKED
+    _require_cuda(table, "table", torch.int32)
+    return ptr(table), table.numel(), 0
+
+
 def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mode=MODE_HOGWILD):
     """Batched train_o2: every walk of ``walks`` [P, L] (int32 rows, -1 = None) in one launch.
 
     node, ctx: float32 CUDA tensors [V, d], updated in place.  seeds: uint64 (stored as int64)
     CUDA tensor [P].  table: uint32 (stored as int32) CUDA tensor [T].  mode: MODE_HOGWILD (all
-    walks in flight, one wavefront each) or MODE_SEQUENTIAL (walks in order: workers=1)."""
+    walks in flight, one wavefront each) or MODE_SEQUENTIAL (walks in order: workers=1).  table
+    may also be a PackedTable (same draws, 16x less table traffic)."""
     import torch
     _require_cuda(node, "node", torch.float32)
     _require_cuda(ctx, "ctx", torch.float32)
     _require_cuda(walks, "walks", torch.int32)
     _require_cuda(seeds, "seeds", torch.int64)
-    _require_cuda(table, "table", torch.int32)
+    tp, T, flag = _table_args(table)
     if node.shape != ctx.shape or node.dim() != 2:
         raise ValueError("node and ctx must both be [V, d]")
     if walks.dim() != 2 or seeds.shape != (walks.shape[0],):
@@ -81,7 +112,7 @@ def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mod
     V, d = node.shape
     rc = _lib.lib().come_sgns_o2(ptr(node), ptr(ctx), V, d, ptr(walks), walks.shape[0],
                                  walks.shape[1], ptr(seeds), int(window), int(negative),
-                                 ptr(table), table.numel(), float(lr), float(alpha), int(mode),
+                                 tp, T, float(lr), float(alpha), int(mode) | flag,
                                  stream_handle(node.device))
     check(rc, "come_sgns_o2")
 
@@ -92,12 +123,12 @@ def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD):
     _require_cuda(node, "node", torch.float32)
     _require_cuda(edges, "edges", torch.int32)
     _require_cuda(seeds, "seeds", torch.int64)
-    _require_cuda(table, "table", torch.int32)
+    tp, T, flag = _table_args(table)
     if edges.dim() != 2 or edges.shape[1] != 2 or seeds.shape != (edges.shape[0],):
         raise ValueError("edges must be [E, 2] and seeds [E]")
     V, d = node.shape
     rc = _lib.lib().come_sgns_o1(ptr(node), V, d, ptr(edges), edges.shape[0], ptr(seeds),
-                                 int(negative), ptr(table), table.numel(), float(lr), int(mode),
+                                 int(negative), tp, T, float(lr), int(mode) | flag,
                                  stream_handle(node.device))
     check(rc, "come_sgns_o1")
 

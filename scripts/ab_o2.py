@@ -46,6 +46,7 @@ def main():
     seeds = torch.from_numpy(tsi.draw_seeds(args.walks).view(np.int64)).to(dev)
     pairs = tsi.count_o2_pairs(walks.cpu().numpy(), 5)
     keys = ["o2_kernel", "o2_blocks_per_cu", "o2_plain_writeback", "o2_waves_per_block"]
+    packed = tsi.pack_table(m.table)  # variant key "packed=1" draws from the packed table
     # warm the tables past the all-zero context rows, then time every launch from that state
     for _ in range(args.warm_launches):
         tsi.sgns_o2(m.node_embedding, m.context_embedding, walks, seeds, 5, args.negative,
@@ -57,12 +58,13 @@ def main():
             opts = parse(v)
             for k in keys:
                 _lib.set_option(k, opts.get(k, 0))
+            table = packed if opts.get("packed", 0) else m.table
             m.node_embedding.copy_(snap[0])
             m.context_embedding.copy_(snap[1])
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             tsi.sgns_o2(m.node_embedding, m.context_embedding, walks, seeds, 5, args.negative,
-                        m.table, 0.025, 1.0, tsi.MODE_HOGWILD)
+                        table, 0.025, 1.0, tsi.MODE_HOGWILD)
             e.record()
             torch.cuda.synchronize()
             if r > 0:  # round 0 = warmup

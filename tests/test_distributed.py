@@ -42,6 +42,18 @@ def _worker(rank, world, port, out_dir):
     before = tables[0].clone()
     sync.sync()
     assert torch.equal(before, tables[0])
+    # overlapped exchange: progress made between start() and finish() is kept, the other
+    # rank's pre-start delta is added exactly once
+    t = torch.from_numpy(np.full((5, 3), 1.0, np.float32))
+    ov = DeltaAllReduce([t])
+    t.add_(float(rank + 1))            # delta before start: rank 0 +1, rank 1 +2
+    ov.start()
+    t.add_(10.0 * (rank + 1))          # progress while the exchange is in flight
+    ov.finish()
+    expect = 1.0 + 1.0 + 2.0 + 10.0 * (rank + 1)
+    assert torch.allclose(t, torch.full_like(t, expect)), (rank, t)
+    ov.sync()                          # then a blocking sync reconciles the replicas
+    assert torch.allclose(t, torch.full_like(t, 1.0 + 3.0 + 30.0)), (rank, t)
     # sharding: every walk exactly once across ranks
     walks = np.arange(101 * 3).reshape(101, 3)
     seeds = np.arange(101)

@@ -371,3 +371,79 @@ def test_karate_flow_deterministic():
     cm = Community2Vec(m, reg_covar=1e-5, lr=float(lr))
     cm.train(list(range(1, 35)), m, float(beta), chunksize=20, iter=5)
     np.testing.assert_allclose(m.node_embedding.cpu().numpy(), z["after_com_node"], atol=1e-5)
+
+
+# ---- packed negative table (come_pack_table) ---------------------------------------------------
+
+def unpack_words(words, T):
+    """Host decode of the packed words: table[64w + i] = base + popcount(bits & (2^(i+1)-1))."""
+    w = words.cpu().numpy().view(np.uint32).reshape(-1, 4)
+    base = w[:, 0].astype(np.int64)
+    bits = (w[:, 3].astype(np.uint64) << np.uint64(32)) | w[:, 2].astype(np.uint64)
+    i = np.arange(64, dtype=np.uint64)
+    on = ((bits[:, None] >> i[None, :]) & np.uint64(1)).astype(np.int64)
+    return (base[:, None] + np.cumsum(on, 1)).reshape(-1)[:T]
+
+
+@pytest.mark.parametrize("V,T", [(34, 5000), (1000, 200000), (3, 64), (7, 50), (5000, 12345),
+                                 (100000, 1000003)])
+def test_pack_table_exact_on_make_table(V, T):
+    rng = np.random.RandomState(V + T)
+    counts = (rng.pareto(1.5, V) * 5 + 1).astype(np.int64)
+    table = orc.make_table(counts, T)
+    p = tsi.pack_table(dev(table))
+    assert p is not None and p.T == T
+    np.testing.assert_array_equal(unpack_words(p.words, T), table.astype(np.int64))
+
+
+def test_pack_table_refuses_non_unit_steps():
+    t = np.arange(0, 300, 2, dtype=np.uint32)  # steps of 2
+    assert tsi.pack_table(dev(t)) is None
+    t = np.array([5, 4, 4, 4], np.uint32)  # decreasing
+    assert tsi.pack_table(dev(t)) is None
+
+
+@pytest.mark.parametrize("d,neg,w,V,L,P,T", [(128, 5, 5, 2000, 80, 40, 100000),
+                                             (2, 4, 3, 34, 20, 20, 5000),
+                                             (256, 10, 5, 500, 60, 10, 64 * 77 + 5),
+                                             (100, 20, 2, 3, 30, 6, 64)])
+def test_o2_o1_packed_table_bit_exact(d, neg, w, V, L, P, T):
+    rng = np.random.RandomState(d + V + T)
+    table = orc.make_table(rng.randint(1, 60, V), T)
+    packed = tsi.pack_table(dev(table))
+    assert packed is not None
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.2, 0.2, (V, d)).astype(np.float32)
+    walks = rng.randint(0, V, (P, L)).astype(np.int32)
+    seeds = rng.randint(0, 2 ** 48, P, dtype=np.int64).astype(np.uint64)
+    node, ctx = dev(node0.copy()), dev(ctx0.copy())
+    tsi.sgns_o2(node, ctx, dev(walks), dev(seeds), w, neg, packed, 0.05, 0.9,
+                tsi.MODE_SEQUENTIAL)
+    n_ref, c_ref = node0.copy(), ctx0.copy()
+    orc.sgns_o2(n_ref, c_ref, walks, seeds, w, neg, table, 0.05, 0.9, dot_mode=orc.DOT_WAVE64)
+    np.testing.assert_array_equal(node.cpu().numpy(), n_ref)
+    np.testing.assert_array_equal(ctx.cpu().numpy(), c_ref)
+    edges = rng.randint(0, V, (3 * P, 2)).astype(np.int32)
+    eseeds = rng.randint(0, 2 ** 48, 3 * P, dtype=np.int64).astype(np.uint64)
+    tsi.sgns_o1(node, dev(edges), dev(eseeds), neg, packed, 0.2, tsi.MODE_SEQUENTIAL)
+    orc.sgns_o1(n_ref, edges, eseeds, neg, table, 0.2, dot_mode=orc.DOT_WAVE64)
+    np.testing.assert_array_equal(node.cpu().numpy(), n_ref)
+
+
+def test_o2_hogwild_packed_equals_plain_when_walks_disjoint():
+    """Hogwild with disjoint walks is deterministic; packed and plain tables give identical
+    tables (same draws)."""
+    rng = np.random.RandomState(3)
+    V, d, P, L = 4000, 128, 64, 40
+    table = orc.make_table(rng.randint(1, 50, V), 100000)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.2, 0.2, (V, d)).astype(np.float32)
+    walks = rng.permutation(V)[:P * L].reshape(P, L).astype(np.int32)
+    seeds = rng.randint(0, 2 ** 48, P, dtype=np.int64).astype(np.uint64)
+    out = []
+    for t in (dev(table), tsi.pack_table(dev(table))):
+        node, ctx = dev(node0.copy()), dev(ctx0.copy())
+        tsi.sgns_o2(node, ctx, dev(walks), dev(seeds), 5, 0, t, 0.05, 1.0, tsi.MODE_HOGWILD)
+        out.append((node.cpu().numpy(), ctx.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
