@@ -129,8 +129,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: blocking delta all-reduce instead of overlapping it with the next "
                          "batch")
-    ap.add_argument("--plain-table", action="store_true",
-                    help="draw negatives from the 400 MB uint32 table instead of its packed form")
+    ap.add_argument("--packed-table", action="store_true",
+                    help="draw negatives from the exact packed table (come_pack_table)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
@@ -181,8 +181,10 @@ def main():
     pairs_per_step = [int(o2_pairs_of_lengths(lengths[s * B:(s + 1) * B], w))
                       for s in range(total_steps)]
     sync = DeltaAllReduce([model.node_embedding, model.context_embedding]) if world > 1 else None
-    # the exact packed negative table (come_pack_table) unless --plain-table
-    neg_table = model.table if args.plain_table else model.negative_table()
+    # the reference's uint32 table, or its exact packed form (come_pack_table) with
+    # --packed-table (same draws; 1% slower at C3 on MI355X, profiles/r01_ab_dynamic_sched.txt)
+    neg_table = model.table_packed if args.packed_table and model.table_packed is not None \
+        else model.table
 
     def step(s):
         tsi.sgns_o2(model.node_embedding, model.context_embedding, walks_all[s * B:(s + 1) * B],

@@ -200,7 +200,8 @@ int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int
 /* ---- Tuning ----
  * Process-wide launch knobs for experiments (0 = automatic): "o2_kernel" (1 direct, 2 ring),
  * "o2_blocks_per_cu", "o2_waves_per_block", "o2_plain_writeback" (1 = Hogwild with plain-store
- * write-back of cached rows: faster but loses concurrent updates; not the default). */
+ * write-back of cached rows: faster but loses concurrent updates; not the default), "o2_static"
+ * (1 = static grid-stride walk assignment instead of the default device work queue). */
 int come_set_option(const char *name, int value);
 
 /* ---- Host helpers ---- */

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 
 #include "come_internal.h"
@@ -34,7 +35,16 @@ static std::once_flag g_once[kMaxDevices];
 static int g_init_rc[kMaxDevices];
 static int g_cus[kMaxDevices];
 
+// Work-queue counters for dynamically scheduled launches: a ring of kCounterSlots int64 per
+// device, allocated once at init; each launch takes the next slot (a launch only touches its own
+// slot, so up to kCounterSlots launches may be in flight on different streams at once).
+static constexpr int kCounterSlots = 256;
+static int64_t *g_counters[kMaxDevices];
+static std::atomic<unsigned> g_counter_next[kMaxDevices];
+
 static void init_device(int dev) {
+    if (hipMalloc((void **)&g_counters[dev], sizeof(int64_t) * kCounterSlots) != hipSuccess)
+        g_counters[dev] = nullptr;
     float tab[kExpTableSize];
     come_exp_table(tab);
     g_init_rc[dev] = come_upload_exp_table(tab);
@@ -55,6 +65,13 @@ int ensure_init(int *device_out) {
 }
 
 int num_cus(int device) { return g_cus[device] > 0 ? g_cus[device] : 256; }
+
+int64_t *launch_counter(int device, void *stream) {
+    if (!g_counters[device]) return nullptr;
+    int64_t *c = g_counters[device] + (g_counter_next[device]++ % kCounterSlots);
+    if (hipMemsetAsync(c, 0, sizeof(int64_t), (hipStream_t)stream) != hipSuccess) return nullptr;
+    return c;
+}
 
 }  // namespace come
 

@@ -21,6 +21,9 @@ int set_error(int code, const char *fmt, ...);  // returns code
 int hip_error(hipError_t e, const char *what);  // returns COME_E_HIP (or OK if e == success)
 int ensure_init(int *device_out);               // come_init() for the current device, once
 int num_cus(int device);                        // multiprocessor count (cached)
+// A zeroed (on `stream`) int64 work-queue counter for one launch, or nullptr (then schedule
+// statically).  Enqueues a hipMemsetAsync: capture-safe.
+int64_t *launch_counter(int device, void *stream);
 
 // Lemire fastmod: a % d for 32-bit a, d >= 1, from one 64-bit multiply-high.  m = 0 encodes
 // "d >= 2^32" (then a % d == a for every 32-bit a).

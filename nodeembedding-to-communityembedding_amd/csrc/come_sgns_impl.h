@@ -221,8 +221,19 @@ struct O2Args {
     float lr;
     float alpha;
     FastMod fm;
-    int packed;  // table points to come_pack_table's words
+    int packed;        // table points to come_pack_table's words
+    int64_t *counter;  // work queue: walks are claimed with atomicAdd (nullptr = grid-stride)
 };
+
+// Next unit of a wavefront: from the launch's work queue (one atomic per unit; a wavefront that
+// starts late -- e.g. its CU was busy with a concurrent RCCL kernel -- simply claims fewer
+// walks) or, without a queue, the static grid-stride sequence.
+__device__ inline int64_t next_unit(int64_t *counter, int64_t cur, int64_t stride, int lane) {
+    if (!counter) return cur + stride;
+    int64_t v = 0;
+    if (lane == 0) v = (int64_t)atomicAdd((unsigned long long *)counter, 1ull);
+    return (int64_t)uniform64((uint64_t)v);  // lane 0 is the first active lane here
+}
 
 // State 64 draws after `base` (lane 63's state advanced once).
 __device__ inline uint64_t advance64(uint64_t base, const LcgLane &lc) {
@@ -429,7 +440,8 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
         return s;
     };
 
-    for (int64_t p = gw; p < a.P; p += nwaves) {
+    for (int64_t p = a.counter ? next_unit(a.counter, 0, 0, lane) : gw; p < a.P;
+         p = next_unit(a.counter, p, nwaves, lane)) {
         const int32_t *__restrict__ walk = a.walks + p * (int64_t)a.L;
         // ---- walk indices: positions [wbase, wbase + 128) in two VGPR chunks ----
         int wbase = 0;

@@ -142,9 +142,13 @@ class Model(object):
             self.table_packed = pack_table(self.table)
 
     def negative_table(self):
-        """What the trainers pass to the kernels: the exact packed form when it exists."""
-        return self.table_packed if getattr(self, "table_packed", None) is not None \
-            else self.table
+        """What the trainers pass to the kernels: the plain uint32 table, or its exact packed
+        form when ``use_packed_table`` is set (same draws; measured 1% slower at C3, where the
+        400 MB table's lines are not the bottleneck -- profiles/r01_ab_*.txt)."""
+        if getattr(self, "use_packed_table", False) and \
+                getattr(self, "table_packed", None) is not None:
+            return self.table_packed
+        return self.table
 
     # ---- persistence ----
     def save(self, path='data', file_name=None):
