@@ -173,13 +173,17 @@ struct DrawBatch {
     int used;         // draws of the batch already consumed (wave-uniform)
 };
 
+// Lanes < count gather their draw's table value (the others hold 0 and must not be consumed).
 template <class Args>
 __device__ inline void draws_fill(DrawBatch &b, uint64_t state0, const LcgLane &lc,
-                                  const Args &a) {
+                                  const Args &a, int count = 64) {
     b.base = state0;
     b.used = 0;
-    const uint64_t s = (lc.a * state0 + lc.c) & kLcgMask;
-    b.target = table_value(a, table_slot(s, a.fm.m, a.fm.d));
+    b.target = 0;
+    if ((int)(threadIdx.x & 63) < count) {
+        const uint64_t s = (lc.a * state0 + lc.c) & kLcgMask;
+        b.target = table_value(a, table_slot(s, a.fm.m, a.fm.d));
+    }
 }
 
 // State of the draw `b.used` positions after the batch base (0 < used <= 64).
@@ -717,7 +721,7 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
         db.used = 0;
         db.base = uniform64(a.seeds[e]);
         db.target = 0;
-        if (n > 0) draws_fill(db, db.base, lc, a);
+        if (n > 0) draws_fill(db, db.base, lc, a, 2 * n);  // only the 2n draws the edge uses
 
         int t1[MAXN + 1], t2[MAXN + 1];
         bool v1[MAXN + 1], v2[MAXN + 1];
