@@ -26,7 +26,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-KERNEL = "come::k_sgns_o2_ring<2, true, 5, true>"  # the launch bench.py times (d=128, n=5, Hogwild)
+def kernel_name(d, n):
+    """The instantiation come_sgns_o2 launches for (d, negative) in Hogwild mode."""
+    vec = 1 if d <= 64 else 2 if d <= 128 else 4 if d <= 256 else 8
+    full = "true" if vec > 1 and d == 64 * vec else "false"
+    maxn = 5 if n <= 5 else 10 if n <= 10 else 20
+    return "come::k_sgns_o2_ring<%d, %s, %d, true>" % (vec, full, maxn)
 
 
 def log(*a):
@@ -258,7 +263,8 @@ def main():
             tj = json.load(open(args.traffic_json))
             if (tj.get("walks_per_launch") == B and tj.get("dim") == d
                     and tj.get("negative") == n
-                    and KERNEL.replace(" ", "") in tj.get("kernel", "").replace(" ", "")):
+                    and kernel_name(d, n).replace(" ", "") in
+                    tj.get("kernel", "").replace(" ", "")):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -286,7 +292,8 @@ def main():
 
     value = total_pairs / elapsed
     out = {
-        "metric": "SGNS pair-updates/sec at d=128, 1M-node graph",
+        "metric": "SGNS pair-updates/sec at d=%d, %s-node graph" % (
+            d, "1M" if V == 1_000_000 else "%gM" % (V / 1e6)),
         "value": value,
         "unit": "pair-updates/s",
         "n_gpus": world,
@@ -300,9 +307,10 @@ def main():
         "data": "synthetic: Chung-Lu power-law graph (gamma 2.5) + uniform random walks, "
                 "tables initialised as the reference (node U(-1,1), ctx 0)",
         "config": {
-            "workload": "configs[2]/C3: O2 SGNS over random walks, power-law %d nodes / %d "
+            "workload": "%s: O2 SGNS over random walks, power-law %d nodes / %d "
                         "edges, d=%d, negative=%d, window=%d, walk_length=%d, table_size=%d" % (
-                            V, g.num_edges, d, n, w, L, args.table_size),
+                            "configs[4]/C5 (one GPU's shard)" if d == 256 and n == 10
+                            else "configs[2]/C3", V, g.num_edges, d, n, w, L, args.table_size),
             "walks_per_step_per_gpu": B,
             "pairs_per_step_per_gpu": pairs_rank_step,
             "sync_every_steps": args.sync_every if world > 1 else None,
@@ -318,7 +326,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": KERNEL,
+            "kernel": kernel_name(d, n),
             "bytes_per_pair": bytes_per_pair,
             "avg_kernel_ms": avg_kernel_s * 1e3,
         },
