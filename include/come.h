@@ -201,7 +201,9 @@ int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int
  * Process-wide launch knobs for experiments (0 = automatic): "o2_kernel" (1 direct, 2 ring),
  * "o2_blocks_per_cu", "o2_waves_per_block", "o2_plain_writeback" (1 = Hogwild with plain-store
  * write-back of cached rows: faster but loses concurrent updates; not the default), "o2_static"
- * (1 = static grid-stride walk assignment instead of the default device work queue). */
+ * (1 = static grid-stride walk assignment instead of the default device work queue),
+ * "o2_pair_atomics" (1 = Hogwild node rows get one float-atomic add per pair instead of one
+ * delta per window residency). */
 int come_set_option(const char *name, int value);
 
 /* ---- Host helpers ---- */

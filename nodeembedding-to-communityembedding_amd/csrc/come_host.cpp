@@ -66,6 +66,23 @@ int ensure_init(int *device_out) {
 
 int num_cus(int device) { return g_cus[device] > 0 ? g_cus[device] : 256; }
 
+// Growable per-device scratch for the O2 ring kernel's entry snapshots (never shrinks; growing
+// frees the old buffer, which waits for the device).
+static float *g_scratch[kMaxDevices];
+static size_t g_scratch_bytes[kMaxDevices];
+static std::mutex g_scratch_mu;
+
+float *o2_scratch(int device, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (g_scratch_bytes[device] >= bytes) return g_scratch[device];
+    if (g_scratch[device]) (void)hipFree(g_scratch[device]);
+    g_scratch[device] = nullptr;
+    g_scratch_bytes[device] = 0;
+    if (hipMalloc((void **)&g_scratch[device], bytes) != hipSuccess) return nullptr;
+    g_scratch_bytes[device] = bytes;
+    return g_scratch[device];
+}
+
 int64_t *launch_counter(int device, void *stream) {
     if (!g_counters[device]) return nullptr;
     int64_t *c = g_counters[device] + (g_counter_next[device]++ % kCounterSlots);

@@ -14,6 +14,7 @@ static int g_opt_o2_blocks_per_cu = 0;  // grid cap override
 static int g_opt_o2_plain_writeback = 0;  // 1 = Hogwild with plain-store write-back (lossy)
 static int g_opt_o2_waves_per_block = 0;
 static int g_opt_o2_static = 0;  // 1 = grid-stride walk assignment instead of the work queue
+static int g_opt_o2_pair_atomics = 0;  // 1 = HOG node rows: one atomic per pair (no snapshots)
 
 // ---- launchers -----------------------------------------------------------------------------
 static const KernelSet &kernel_set(int d, int *full) {
@@ -98,7 +99,7 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
     if (!aligned_for(node, d) || !aligned_for(ctx, d))
         return set_error(COME_E_INVALID, "node/ctx must be 16-byte aligned for d=%d", d);
     O2Args a{node, ctx, walks, seeds, table, V, P, L, d, window, negative, lr, alpha,
-             make_fastmod(T), packed, nullptr};
+             make_fastmod(T), packed, nullptr, nullptr};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
     const int mi = maxn_index(negative);
@@ -117,11 +118,18 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
         per_cu = per_cu < 1 ? 1 : (per_cu > 24 / wpb ? 24 / wpb : per_cu);
         if (g_opt_o2_blocks_per_cu > 0) per_cu = g_opt_o2_blocks_per_cu;
         const int variant = (hog && !g_opt_o2_plain_writeback) ? 1 : 0;
-        if (hog && !g_opt_o2_static) {
+        if (hog) {
             int dev = 0;
             rc = ensure_init(&dev);
             if (rc) return rc;
-            a.counter = launch_counter(dev, stream);  // nullptr -> grid-stride fallback
+            if (!g_opt_o2_static) a.counter = launch_counter(dev, stream);  // else grid-stride
+            if (variant == 1 && !g_opt_o2_pair_atomics) {
+                // entry snapshots, one [2w+1][d] region per wavefront of the (capped) grid
+                int64_t blocks = (P + wpb - 1) / wpb;
+                const int64_t cap = (int64_t)num_cus(dev) * per_cu;
+                if (blocks > cap) blocks = cap;
+                a.orig = o2_scratch(dev, (size_t)blocks * wpb * rs * d * sizeof(float));
+            }
         }
         return launch(ks.o2_ring[full][mi][variant], &a, P, mode, wpb, per_cu, lds, stream);
     }
@@ -211,7 +219,8 @@ extern "C" int come_set_option(const char *name, int value) {
                 {"o2_blocks_per_cu", &g_opt_o2_blocks_per_cu},
                 {"o2_plain_writeback", &g_opt_o2_plain_writeback},
                 {"o2_waves_per_block", &g_opt_o2_waves_per_block},
-                {"o2_static", &g_opt_o2_static}};
+                {"o2_static", &g_opt_o2_static},
+                {"o2_pair_atomics", &g_opt_o2_pair_atomics}};
     for (auto &o : opts)
         if (!strcmp(o.k, name)) {
             *o.v = value;

@@ -227,6 +227,9 @@ struct O2Args {
     FastMod fm;
     int packed;        // table points to come_pack_table's words
     int64_t *counter;  // work queue: walks are claimed with atomicAdd (nullptr = grid-stride)
+    float *orig;       // HOG, optional: per-wavefront [2w+1][d] entry snapshots of the ring rows
+                       // (node rows then get ONE atomic delta when they leave the window instead
+                       // of one atomic per pair); nullptr = per-pair atomics
 };
 
 // Next unit of a wavefront: from the launch's work queue (one atomic per unit; a wavefront that
@@ -503,21 +506,35 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
             return __ballot(lane < RS && lane != except && ids == id);
         };
         auto set_id = [&](int s, int id) { ids = lane == s ? id : ids; };
-        auto write_back = [&](int s, int id) {  // SEQ: last holder stores the row
-            if (!HOG && alias_mask(id, s) == 0) {
+        float *orig = HOG && a.orig ? a.orig + gw * (int64_t)RS * d : nullptr;
+        auto write_back = [&](int s, int id) {  // the last holder of a node row writes it back
+            if (alias_mask(id, s) != 0) return;
+            if (!HOG) {  // SEQ: plain store
                 R row;
                 row.load(ring + s * d, lane, d);
                 row.store(a.node + (int64_t)id * d, lane, d);
+            } else if (orig) {  // HOG, delta-at-exit: node[id] += cur - entry snapshot
+                R row, o;
+                row.load(ring + s * d, lane, d);
+                o.load(orig + s * d, lane, d);
+                atomic_add_delta(a.node + (int64_t)id * d, row, o, lane, d);
             }
         };
         auto enter_row = [&](int s, int id, const R &fetched) {  // fetched: node[id] loaded earlier
             const uint64_t m = alias_mask(id, s);
             if (m) {
                 R row;
-                row.load(ring + __builtin_ctzll(m) * d, lane, d);
+                const int src = __builtin_ctzll(m);
+                row.load(ring + src * d, lane, d);
                 row.store(ring + s * d, lane, d);
+                if (orig) {  // every alias carries the snapshot of the id's first entry
+                    R o;
+                    o.load(orig + src * d, lane, d);
+                    o.store(orig + s * d, lane, d);
+                }
             } else {
                 fetched.store(ring + s * d, lane, d);
+                if (orig) fetched.store(orig + s * d, lane, d);
             }
             set_id(s, id);
         };
@@ -656,7 +673,7 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
                     }
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) in.v[e] = in.v[e] + work.v[e];  // pyx:149
-                    if (HOG) work.atomic_add(a.node + (int64_t)cj * d, lane, d);
+                    if (HOG && !orig) work.atomic_add(a.node + (int64_t)cj * d, lane, d);
                     uint64_t m = alias_mask(cj, -1);  // the slot and every alias of it
                     while (m) {
                         const int rr = __builtin_ctzll(m);
