@@ -273,7 +273,14 @@ def main():
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="come_set_option knob, e.g. --opt o1_pipe=0 (A/B experiments)")
     args = ap.parse_args()
+    if args.opt:
+        from come_amd import _lib
+        for kv in args.opt:
+            k, v = kv.split("=")
+            _lib.set_option(k, int(v))
     {"c2": c2, "c4": c4, "walks": walks}[args.workload](args)
 
 

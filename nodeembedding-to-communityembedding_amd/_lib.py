@@ -44,6 +44,9 @@ def lib():
         raise ComeError("libcome.so not found at %s -- build it with "
                         "`make -C nodeembedding-to-communityembedding_amd/csrc` or "
                         "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+    # torch first: it ships its own HIP runtime, and libcome.so must bind to that same instance
+    # (loaded first, libcome would pull /opt/rocm's copy and torch would then see no device)
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     P, i32, i64, u64, f32, f64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
                                   ctypes.c_float, ctypes.c_double)

@@ -8,6 +8,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <unordered_map>
 
 #include "come_internal.h"
 
@@ -66,21 +67,28 @@ int ensure_init(int *device_out) {
 
 int num_cus(int device) { return g_cus[device] > 0 ? g_cus[device] : 256; }
 
-// Growable per-device scratch for the O2 ring kernel's entry snapshots (never shrinks; growing
-// frees the old buffer, which waits for the device).
-static float *g_scratch[kMaxDevices];
-static size_t g_scratch_bytes[kMaxDevices];
+// Growable scratch for the O2 ring kernel's entry snapshots, one buffer per (device, stream) so
+// launches on different streams never share snapshot regions (never shrinks; growing frees the
+// old buffer, which waits for the device).
+struct Scratch {
+    float *ptr = nullptr;
+    size_t bytes = 0;
+};
+static std::unordered_map<void *, Scratch> g_scratch[kMaxDevices];
 static std::mutex g_scratch_mu;
 
-float *o2_scratch(int device, size_t bytes) {
+float *o2_scratch(int device, void *stream, size_t bytes) {
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    if (g_scratch_bytes[device] >= bytes) return g_scratch[device];
-    if (g_scratch[device]) (void)hipFree(g_scratch[device]);
-    g_scratch[device] = nullptr;
-    g_scratch_bytes[device] = 0;
-    if (hipMalloc((void **)&g_scratch[device], bytes) != hipSuccess) return nullptr;
-    g_scratch_bytes[device] = bytes;
-    return g_scratch[device];
+    Scratch &s = g_scratch[device][stream];
+    if (s.bytes >= bytes) return s.ptr;
+    if (s.ptr) (void)hipFree(s.ptr);
+    s = Scratch{};
+    if (hipMalloc((void **)&s.ptr, bytes) != hipSuccess) {
+        s.ptr = nullptr;
+        return nullptr;
+    }
+    s.bytes = bytes;
+    return s.ptr;
 }
 
 int64_t *launch_counter(int device, void *stream) {

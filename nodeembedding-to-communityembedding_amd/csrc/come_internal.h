@@ -24,9 +24,10 @@ int num_cus(int device);                        // multiprocessor count (cached)
 // A zeroed (on `stream`) int64 work-queue counter for one launch, or nullptr (then schedule
 // statically).  Enqueues a hipMemsetAsync: capture-safe.
 int64_t *launch_counter(int device, void *stream);
-// Device scratch of at least `bytes` (library-owned, grows on demand: the first call at a larger
-// size allocates, so capture a stream only after a warm-up call of the same shape).
-float *o2_scratch(int device, size_t bytes);
+// Device scratch of at least `bytes` for launches on `stream` (library-owned, one buffer per
+// device and stream, grows on demand: the first call at a larger size allocates, so capture a
+// stream only after a warm-up call of the same shape).
+float *o2_scratch(int device, void *stream, size_t bytes);
 
 // Lemire fastmod: a % d for 32-bit a, d >= 1, from one 64-bit multiply-high.  m = 0 encodes
 // "d >= 2^32" (then a % d == a for every 32-bit a).

@@ -113,7 +113,8 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
         const int wpb = g_opt_o2_waves_per_block == 1 ? 1 : 2;
         const size_t lds = wave_bytes * (hog ? wpb : 1);
         // 24 wavefronts per CU measured best on MI355X (d=128, n=5: 16/20/24/28 waves ->
-        // 141/123/110/132 ms per 1e8-pair launch, scripts/ab_o2.py): more in flight thrashes.
+        // 141/123/110/132 ms per 1e8-pair launch with the first write-back; with the work queue
+        // and delta write-back 20/22/24/26 -> 111.0/104.6/100.3/100.3 ms, scripts/ab_o2.py).
         int per_cu = (int)(kLdsPerCu / (wave_bytes * wpb));
         per_cu = per_cu < 1 ? 1 : (per_cu > 24 / wpb ? 24 / wpb : per_cu);
         if (g_opt_o2_blocks_per_cu > 0) per_cu = g_opt_o2_blocks_per_cu;
@@ -128,7 +129,7 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
                 int64_t blocks = (P + wpb - 1) / wpb;
                 const int64_t cap = (int64_t)num_cus(dev) * per_cu;
                 if (blocks > cap) blocks = cap;
-                a.orig = o2_scratch(dev, (size_t)blocks * wpb * rs * d * sizeof(float));
+                a.orig = o2_scratch(dev, stream, (size_t)blocks * wpb * rs * d * sizeof(float));
             }
         }
         return launch(ks.o2_ring[full][mi][variant], &a, P, mode, wpb, per_cu, lds, stream);
