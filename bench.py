@@ -271,7 +271,7 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        sample = B  # ~1e8 pairs: the deadline (--cpu-seconds), not the sample, ends the run
+        sample = min(2 * B, walks_all.shape[0])  # ~2e8 pairs: the deadline ends the run
         wn = walks_all[:sample].cpu().numpy()
         node_h = np.ascontiguousarray(model.node_embedding.cpu().numpy())
         ctx_h = np.ascontiguousarray(model.context_embedding.cpu().numpy())
