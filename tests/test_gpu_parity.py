@@ -447,3 +447,105 @@ def test_o2_hogwild_packed_equals_plain_when_walks_disjoint():
         out.append((node.cpu().numpy(), ctx.cpu().numpy()))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+# ---- edge shapes and sizes ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("case", ["empty_batch", "single_node_walks", "window_gt_len",
+                                  "all_none", "d512", "d257", "one_walk_long", "V1"])
+def test_o2_edge_shapes_bit_exact(case):
+    """Empty batch, length-1 walks (no pairs), window wider than the walk, walks of None only,
+    the widest rows (d = 512, one 2-KB row per 4 wave instructions) and a masked odd width
+    (d = 257), one long walk, a one-node vocabulary (every draw collides with the positive)."""
+    rng = np.random.RandomState(hash(case) % 1000)
+    d, neg, w, V, L, P = {"empty_batch": (128, 5, 5, 50, 10, 0),
+                          "single_node_walks": (128, 5, 5, 50, 1, 7),
+                          "window_gt_len": (64, 3, 9, 40, 6, 9),
+                          "all_none": (128, 5, 5, 50, 20, 3),
+                          "d512": (512, 4, 3, 60, 25, 6),
+                          "d257": (257, 2, 2, 30, 15, 5),
+                          "one_walk_long": (128, 5, 5, 500, 4000, 1),
+                          "V1": (16, 5, 2, 1, 12, 3)}[case]
+    table = orc.make_table(rng.randint(1, 30, V), 997) if V > 1 else np.zeros(97, np.uint32)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.2, 0.2, (V, d)).astype(np.float32)
+    walks = rng.randint(0, V, (P, L)).astype(np.int32)
+    if case == "all_none":
+        walks[:] = -1
+    seeds = rng.randint(0, 2 ** 48, P, dtype=np.int64).astype(np.uint64)
+    for mode in (tsi.MODE_SEQUENTIAL, tsi.MODE_HOGWILD):
+        node, ctx = dev(node0.copy()), dev(ctx0.copy())
+        tsi.sgns_o2(node, ctx, dev(walks.reshape(P, L)), dev(seeds), w, neg, dev(table), 0.05,
+                    1.0, mode)
+        n_ref, c_ref = node0.copy(), ctx0.copy()
+        if P:
+            orc.sgns_o2(n_ref, c_ref, walks, seeds, w, neg, table, 0.05, 1.0,
+                        dot_mode=orc.DOT_WAVE64)
+        if mode == tsi.MODE_SEQUENTIAL:
+            np.testing.assert_array_equal(node.cpu().numpy(), n_ref)
+            np.testing.assert_array_equal(ctx.cpu().numpy(), c_ref)
+        elif P <= 1:  # one walk in flight: sequential up to the rounding of the atomic delta
+            # write-back, which over a 4000-step walk can flip sigmoid buckets: tier B, 1e-3
+            np.testing.assert_allclose(node.cpu().numpy(), n_ref, rtol=0, atol=1e-3)
+            np.testing.assert_allclose(ctx.cpu().numpy(), c_ref, rtol=0, atol=1e-3)
+        else:
+            assert torch.isfinite(node).all() and torch.isfinite(ctx).all()
+    if case in ("empty_batch", "single_node_walks", "all_none"):
+        np.testing.assert_array_equal(n_ref, node0)
+
+
+def test_o2_o1_rows_beyond_2_32_elements():
+    """Rows whose element offset exceeds 2^32 (V x d > 4.29e9: the reference's 32-bit
+    `word2_index * size` would wrap, the kernels use 64-bit offsets).  Compact problem on the
+    host oracle, the same problem scattered onto rows >= 2^32 / d of 17 GB device tables:
+    touched rows bit-identical."""
+    d, Vc, V = 256, 40, 16_800_000
+    if torch.cuda.get_device_properties(0).total_memory < 48 * 2 ** 30:
+        pytest.skip("needs ~36 GB of device memory")
+    rng = np.random.RandomState(7)
+    big = np.sort(rng.choice(np.arange(2 ** 32 // d - 20, V), Vc, replace=False)).astype(np.int64)
+    assert big[-1] * d > 2 ** 32
+    table_c = orc.make_table(rng.randint(1, 20, Vc), 3001)
+    node0 = rng.uniform(-1, 1, (Vc, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.2, 0.2, (Vc, d)).astype(np.float32)
+    walks_c = rng.randint(0, Vc, (6, 30)).astype(np.int32)
+    edges_c = rng.randint(0, Vc, (20, 2)).astype(np.int32)
+    seeds = rng.randint(0, 2 ** 48, 6, dtype=np.int64).astype(np.uint64)
+    eseeds = rng.randint(0, 2 ** 48, 20, dtype=np.int64).astype(np.uint64)
+    n_ref, c_ref = node0.copy(), ctx0.copy()
+    orc.sgns_o2(n_ref, c_ref, walks_c, seeds, 5, 5, table_c, 0.05, 1.0, dot_mode=orc.DOT_WAVE64)
+    orc.sgns_o1(n_ref, edges_c, eseeds, 5, table_c, 0.2, dot_mode=orc.DOT_WAVE64)
+    node = torch.zeros((V, d), dtype=torch.float32, device=DEV)
+    ctx = torch.zeros((V, d), dtype=torch.float32, device=DEV)
+    bi = torch.from_numpy(big).to(DEV)
+    node[bi] = dev(node0)
+    ctx[bi] = dev(ctx0)
+    try:
+        tsi.sgns_o2(node, ctx, dev(big[walks_c].astype(np.int32)), dev(seeds), 5, 5,
+                    dev(big[table_c].astype(np.uint32)), 0.05, 1.0, tsi.MODE_SEQUENTIAL)
+        tsi.sgns_o1(node, dev(big[edges_c].astype(np.int32)), dev(eseeds), 5,
+                    dev(big[table_c].astype(np.uint32)), 0.2, tsi.MODE_SEQUENTIAL)
+        np.testing.assert_array_equal(node[bi].cpu().numpy(), n_ref)
+        np.testing.assert_array_equal(ctx[bi].cpu().numpy(), c_ref)
+    finally:
+        del node, ctx
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("w", [1, 2, 5])
+def test_o2_hogwild_single_walk_sees_its_own_writebacks(w):
+    """One walk in flight, nodes that leave the window and re-enter at the very next boundary
+    (period 2w + 2) and centers whose positive row comes back as a later positive: the
+    wavefront must read back its own atomic write-backs (no stale L1 line), so Hogwild equals
+    the sequential run up to the rounding of row += (cur - orig): <= 1e-5 abs over a short walk."""
+    rng = np.random.RandomState(w)
+    V, d, L = 2 * w + 2, 128, 6 * (2 * w + 2)
+    table = np.zeros(1, np.uint32)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    ctx0 = rng.uniform(-0.5, 0.5, (V, d)).astype(np.float32)
+    walks = np.resize(rng.permutation(V), L).reshape(1, L).astype(np.int32)
+    seeds = np.zeros(1, np.uint64)
+    h = run_o2(node0, ctx0, walks, seeds, w, 0, table, 0.1, 1.0, tsi.MODE_HOGWILD)
+    s = run_o2(node0, ctx0, walks, seeds, w, 0, table, 0.1, 1.0, tsi.MODE_SEQUENTIAL)
+    np.testing.assert_allclose(h[0], s[0], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(h[1], s[1], rtol=0, atol=1e-5)
