@@ -108,7 +108,8 @@ int come_community_grad(float *x, int64_t V, int d, const float *pi, const float
  * for covariance_type='full'.  prec_chol [K x d x d] (precision Cholesky factors, sklearn
  * layout), mu_prec [K x d] = mu_k @ prec_chol_k, log_norm [K] = log w_k + log det(prec_chol_k)
  * - d/2 log(2 pi) (all device fp32, precomputed on the host from the fitted parameters).
- * resp_out [V x K] device fp32.  K <= 64. */
+ * resp_out [V x K] device fp32.  K <= 64 (K <= 4096 for d = 64, 128: the MFMA path keeps the
+ * per-component log-probabilities in resp_out itself). */
 int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
                   const float *log_norm, int K, float *resp_out, void *stream);
 
@@ -203,7 +204,10 @@ int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int
  * write-back of cached rows: faster but loses concurrent updates; not the default), "o2_static"
  * (1 = static grid-stride walk assignment instead of the default device work queue),
  * "o2_pair_atomics" (1 = Hogwild node rows get one float-atomic add per pair instead of one
- * delta per window residency). */
+ * delta per window residency), "rows_per_wave" / "o1_rows_per_wave" (Hogwild launches keep at
+ * most V / rows_per_wave wavefronts in flight so updates stay sparse on small vocabularies;
+ * defaults 16 / 12, 0 = no cap), "max_waves" (absolute cap on wavefronts in flight, 0 = none).
+ * Note: come_set_option() returns to the default only when set to the default value. */
 int come_set_option(const char *name, int value);
 
 /* ---- Host helpers ---- */

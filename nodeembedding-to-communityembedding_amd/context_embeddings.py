@@ -34,8 +34,9 @@ class Context2Vec(object):
         self.batch_walks = int(batch_walks)
 
     def train(self, model, paths, total_nodes, alpha=1.0, node_count=0, chunksize=150):
-        """Train the context embedding on ``paths`` (iterable of node-id walks or a [P, L] id
-        array).  Returns the number of pair updates performed."""
+        """Train the context embedding on ``paths`` (iterable of node-id walks, a [P, L] id
+        array, or a CUDA id tensor [P, L] with -1 after each walk's end -- converted and trained
+        without leaving the device).  Returns the number of pair updates performed."""
         import torch
         assert model.node_embedding.dtype == torch.float32
         assert model.context_embedding.dtype == torch.float32
@@ -46,17 +47,27 @@ class Context2Vec(object):
         start = time.time()
         rows = walks_to_rows(model, paths, max_len=tsi.MAX_SENTENCE_LEN)
         seeds = tsi.draw_seeds(rows.shape[0])
-        pairs = tsi.count_o2_pairs(rows, self.window_size)
         dev = model.node_embedding.device
+        if isinstance(rows, torch.Tensor):  # device walks: count on the device
+            lens = (rows >= 0).sum(dim=1).long()
+            w_ = self.window_size
+            pairs = int(torch.where(lens >= w_ + 1, 2 * w_ * lens - w_ * (w_ + 1),
+                                    lens * (lens - 1)).sum())
+            n_valid = int(lens.sum())
+        else:
+            pairs = tsi.count_o2_pairs(rows, self.window_size)
+            n_valid = int((rows >= 0).sum())
         mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
         for s in range(0, rows.shape[0], self.batch_walks):
-            w = torch.from_numpy(np.ascontiguousarray(rows[s:s + self.batch_walks])).to(dev)
+            w = rows[s:s + self.batch_walks]
+            w = w.contiguous() if isinstance(w, torch.Tensor) else \
+                torch.from_numpy(np.ascontiguousarray(w)).to(dev)
             sd = torch.from_numpy(seeds[s:s + self.batch_walks].view(np.int64)).to(dev)
             tsi.sgns_o2(model.node_embedding, model.context_embedding, w, sd, self.window_size,
                         self.negative, model.negative_table(), self.lr, alpha, mode)
         torch.cuda.synchronize(dev)
         elapsed = time.time() - start
-        nodes = int((rows >= 0).sum()) + node_count
+        nodes = n_valid + node_count
         log.info("O2 training on %i nodes (%i pair updates) took %.2fs, %.0f pairs/s",
                  nodes, pairs, elapsed, pairs / elapsed if elapsed else 0.0)
         return pairs

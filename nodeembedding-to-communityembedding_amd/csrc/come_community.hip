@@ -493,8 +493,10 @@ extern "C" int come_gmm_resp(const float *x, int64_t V, int d, const float *prec
 extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol,
                               const float *mu_prec, const float *log_norm, int K, float *resp_out,
                               float *lse_out, void *stream) {
-    if (V < 0 || d < 1 || d > 128 || K < 1 || K > 64)
-        return set_error(COME_E_INVALID, "gmm_resp: need V>=0, 1<=d<=128, 1<=K<=64");
+    const bool mfma = (d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0;
+    if (V < 0 || d < 1 || d > 128 || K < 1 || K > 4096 || (!mfma && K > 64))
+        return set_error(COME_E_INVALID, "gmm_resp: need V>=0, 1<=d<=128, 1<=K<=64 (K<=4096 "
+                                         "for d = 64, 128)");
     if (V == 0) return COME_OK;
     if (!x || !prec_chol || !mu_prec || !log_norm || !resp_out)
         return set_error(COME_E_INVALID, "null pointer");
@@ -502,7 +504,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
     int rc = ensure_init(&dev);
     if (rc) return rc;
     RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K};
-    if ((d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0) {
+    if (mfma) {
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(d * d + d);
         void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_mfma<64> : k_gmm_resp_mfma<128>;

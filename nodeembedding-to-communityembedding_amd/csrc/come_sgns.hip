@@ -15,6 +15,25 @@ static int g_opt_o2_plain_writeback = 0;  // 1 = Hogwild with plain-store write-
 static int g_opt_o2_waves_per_block = 0;
 static int g_opt_o2_static = 0;  // 1 = grid-stride walk assignment instead of the work queue
 static int g_opt_o2_pair_atomics = 0;  // 1 = HOG node rows: one atomic per pair (no snapshots)
+// Hogwild concurrency: at most max(1, V / rows_per_wave) wavefronts in flight (0 = no V-based
+// cap) and at most max_waves (0 = the hardware's occupancy).  Hogwild needs sparse updates: with
+// every wavefront holding ~17 rows (O2: the 2w+1 window, the positive, the pair's negatives; O1
+// 12), a vocabulary smaller than ~16 rows per wavefront in flight has most rows held by several
+// wavefronts at once and the embeddings stop converging -- measured on a 2,000-node planted
+// partition (scripts/diag_hogwild.py): community NMI 0.75 with 6,000 waves in flight, 0.97-0.98
+// with <= V/16 (= the sequential run's 0.97); at 100,000 nodes the cap is inactive (V/16 >
+// occupancy) and NMI 0.99 either way.
+static int g_opt_rows_per_wave = 16;     // O2
+static int g_opt_o1_rows_per_wave = 12;  // O1
+static int g_opt_max_waves = 0;
+
+// Cap on the number of workgroups of a Hogwild launch (0 = none).
+static int64_t hog_max_blocks(int64_t V, int wpb, int rows_per_wave) {
+    int64_t waves = 0;
+    if (rows_per_wave > 0) waves = V / rows_per_wave > 1 ? V / rows_per_wave : 1;
+    if (g_opt_max_waves > 0 && (waves == 0 || g_opt_max_waves < waves)) waves = g_opt_max_waves;
+    return waves > 0 ? (waves + wpb - 1) / wpb : 0;
+}
 
 // ---- launchers -----------------------------------------------------------------------------
 static const KernelSet &kernel_set(int d, int *full) {
@@ -32,7 +51,7 @@ static int maxn_index(int n) { return n <= 5 ? 0 : (n <= 10 ? 1 : 2); }
 // Launch `fn` with one wavefront per unit (walk / edge), `wpb` wavefronts per workgroup, grid
 // capped at `blocks_per_cu` workgroups per CU (grid-stride beyond); SEQUENTIAL = one wavefront.
 static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int blocks_per_cu,
-                  size_t lds_bytes, void *stream) {
+                  size_t lds_bytes, void *stream, int64_t max_blocks = 0) {
     int dev = 0;
     int rc = ensure_init(&dev);
     if (rc) return rc;
@@ -42,7 +61,8 @@ static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int bl
         block = dim3(64);
     } else {
         int64_t blocks = (units + wpb - 1) / wpb;
-        const int64_t cap = (int64_t)num_cus(dev) * blocks_per_cu;
+        int64_t cap = (int64_t)num_cus(dev) * blocks_per_cu;
+        if (max_blocks > 0 && max_blocks < cap) cap = max_blocks;
         if (blocks > cap) blocks = cap;
         grid = dim3((unsigned)(blocks > 0 ? blocks : 1));
         block = dim3(64 * wpb);
@@ -127,15 +147,19 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
             if (variant == 1 && !g_opt_o2_pair_atomics) {
                 // entry snapshots, one [2w+1][d] region per wavefront of the (capped) grid
                 int64_t blocks = (P + wpb - 1) / wpb;
-                const int64_t cap = (int64_t)num_cus(dev) * per_cu;
+                int64_t cap = (int64_t)num_cus(dev) * per_cu;
+                const int64_t hcap = hog_max_blocks(V, wpb, g_opt_rows_per_wave);
+                if (hcap > 0 && hcap < cap) cap = hcap;
                 if (blocks > cap) blocks = cap;
                 a.orig = o2_scratch(dev, stream, (size_t)blocks * wpb * rs * d * sizeof(float));
             }
         }
-        return launch(ks.o2_ring[full][mi][variant], &a, P, mode, wpb, per_cu, lds, stream);
+        return launch(ks.o2_ring[full][mi][variant], &a, P, mode, wpb, per_cu, lds, stream,
+                      hog ? hog_max_blocks(V, wpb, g_opt_rows_per_wave) : 0);
     }
     return launch(ks.o2_direct[full][mi], &a, P, mode, 4,
-                  g_opt_o2_blocks_per_cu > 0 ? g_opt_o2_blocks_per_cu : 6, 0, stream);
+                  g_opt_o2_blocks_per_cu > 0 ? g_opt_o2_blocks_per_cu : 6, 0, stream,
+                  hog ? hog_max_blocks(V, 4, g_opt_rows_per_wave) : 0);
 }
 
 extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
@@ -154,7 +178,8 @@ extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges,
     O1Args a{node, edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
-    return launch(ks.o1[full][maxn_index(negative)], &a, E, mode, 4, 8, 0, stream);
+    return launch(ks.o1[full][maxn_index(negative)], &a, E, mode, 4, 8, 0, stream,
+                  mode == COME_MODE_HOGWILD ? hog_max_blocks(V, 4, g_opt_o1_rows_per_wave) : 0);
 }
 
 // One wavefront per 64-slot word: lane i loads slot 64w + i (one coalesced 256-B read), the
@@ -221,7 +246,10 @@ extern "C" int come_set_option(const char *name, int value) {
                 {"o2_plain_writeback", &g_opt_o2_plain_writeback},
                 {"o2_waves_per_block", &g_opt_o2_waves_per_block},
                 {"o2_static", &g_opt_o2_static},
-                {"o2_pair_atomics", &g_opt_o2_pair_atomics}};
+                {"o2_pair_atomics", &g_opt_o2_pair_atomics},
+                {"rows_per_wave", &g_opt_rows_per_wave},
+                {"o1_rows_per_wave", &g_opt_o1_rows_per_wave},
+                {"max_waves", &g_opt_max_waves}};
     for (auto &o : opts)
         if (!strcmp(o.k, name)) {
             *o.v = value;

@@ -69,6 +69,31 @@ class RepeatCorpusNTimes():
                 yield document
 
 
+def _device_rows(model, ids, max_len):
+    """CUDA id tensor [P, L] -> CUDA int32 rows, or None when the host path is needed (OOV ids
+    inside a walk must be dropped and the walk compacted; down-sampling draws on the host)."""
+    import torch
+    if model.down_sampling or ids.dim() != 2:
+        return None
+    ids = ids.long()
+    if model._contiguous:
+        rows = torch.where((ids >= 1) & (ids <= model.vocab_size), ids - 1,
+                           torch.full_like(ids, -1))
+    else:
+        nid = torch.from_numpy(model.node_ids).to(ids.device)
+        pos = torch.searchsorted(nid, ids).clamp_max(model.vocab_size - 1)
+        rows = torch.where(nid[pos] == ids, pos, torch.full_like(ids, -1))
+    if bool(((rows < 0) & (ids >= 0)).any()):
+        return None  # OOV inside a walk
+    valid = rows >= 0
+    # trailing padding only (a valid entry after a -1 would need compaction)
+    if ids.shape[1] > 1 and bool((valid[:, 1:] & ~valid[:, :-1]).any()):
+        return None
+    if max_len is not None and rows.shape[1] > max_len:
+        rows = rows[:, :max_len]
+    return rows.to(torch.int32).contiguous()
+
+
 def walks_to_rows(model, paths, max_len=None):
     """Vectorised prepare_sentences for the batched kernels.
 
@@ -76,7 +101,14 @@ def walks_to_rows(model, paths, max_len=None):
     Returns an int32 array [P, Lmax] of row indices, OOV ids dropped (as prepare_sentences does),
     ragged rows padded with -1 (train_o2 treats trailing None exactly like a shorter path).
     Down-sampling (model.down_sampling > 0) draws one np.random.random_sample per in-vocabulary
-    node whose sample_probability < 1, walk by walk, node by node."""
+    node whose sample_probability < 1, walk by walk, node by node.
+    A CUDA tensor of node ids (e.g. come_amd.graph_utils.device_walks output mapped to ids, -1
+    after a walk's end) is converted on the device and returned as a CUDA int32 tensor."""
+    if hasattr(paths, "is_cuda") and paths.is_cuda:
+        rows = _device_rows(model, paths, max_len)
+        if rows is not None:
+            return rows
+        paths = paths.cpu().numpy()
     if isinstance(paths, np.ndarray) and paths.ndim == 2:
         rows = model.rows_of(paths.reshape(-1)).reshape(paths.shape)
         if not model.down_sampling and (rows >= 0).all():
