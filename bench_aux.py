@@ -129,11 +129,28 @@ def c2(args):
 
 
 def c4(args):
+    """N = 1: the three kernels on all V rows.  N > 1 (torchrun, one rank per GPU):
+    every rank owns V/N rows of the replicated tables; a community pass = the kernel on the rank's
+    rows + one all-gather of the updated rows (RCCL), an EM iteration = local E-step + M-step with
+    the sufficient statistics all-reduced (come_amd.gmm distributed=True).  value = all ranks'
+    flops / max-over-ranks time (strong scaling: V is fixed)."""
     import torch
+    import torch.distributed as dist
     from come_amd import community_embeddings as ce
+    from come_amd.distributed import all_gather_rows, shard_range
     from oracle import oracle as orc
-    dev = torch.device("cuda", 0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if args.all_ranks_device0 else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     V, K, d = args.nodes, args.k, args.dim
+    lo, hi = shard_range(V, rank, world)
     rng = np.random.RandomState(2)
     x = torch.from_numpy(rng.standard_normal((V, d)).astype(np.float32)).to(dev)
     A = rng.standard_normal((K, d, d)) / np.sqrt(d)
@@ -147,26 +164,44 @@ def c4(args):
                                     orc.precision_cholesky(cov), dev)
     flops = 2.0 * V * K * d * d
     x0 = x.clone()
-    el_g, ks_g = timed(lambda: ce.community_grad(x, pi, mu, inv, 0.01, 0.1, 1), args.steps,
-                       args.warmup)
-    el_r, ks_r = timed(lambda: ce.gmm_resp(x0, pc, mp, ln), args.steps, args.warmup)
+    xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]
+
+    def community_pass():
+        ce.community_grad(xs, pis, mu, inv, 0.01, 0.1, 1)
+        if world > 1:
+            all_gather_rows(x)
+    if world > 1:  # kernel alone on the rank's rows (the exchange excluded)
+        _, ks_k = timed(lambda: ce.community_grad(xs, pis, mu, inv, 0.01, 0.1, 1), args.steps,
+                        args.warmup)
+    el_g, ks_g = timed(community_pass, args.steps, args.warmup)
+    el_r, ks_r = timed(lambda: ce.gmm_resp(x0s, pc, mp, ln), args.steps, args.warmup)
     tg, tr = float(np.mean(ks_g)) / 1e3, float(np.mean(ks_r)) / 1e3
     # one GMM EM iteration (come_amd.gmm: E-step kernel + means GEMM + scatter kernel + K
     # Cholesky factorisations), and the M-step scatter kernel alone
     from come_amd import gmm
-    gm = gmm.GaussianMixture(K, reg_covar=1e-5)
+    gm = gmm.GaussianMixture(K, reg_covar=1e-5, distributed=world > 1)
+    gm._n_total = V
     t64 = lambda a: torch.as_tensor(np.asarray(a, np.float64), device=dev)  # noqa: E731
     gm._set_params(t64(w), mu.double(), t64(cov))
-    resp0 = pi.contiguous()
+    resp0 = pis.contiguous()
 
     def em_iter():
-        resp, _ = gmm.estep(x0, gm._e_pc, gm._e_mp, gm._e_ln)
-        gm._set_params(*gm._m_step(x0, resp))
+        resp, _ = gmm.estep(x0s, gm._e_pc, gm._e_mp, gm._e_ln)
+        gm._set_params(*gm._m_step(x0s, resp))
     el_e, ks_e = timed(em_iter, args.steps, args.warmup)
-    el_s, ks_s = timed(lambda: gmm.scatter(x0, resp0, mu), args.steps, args.warmup)
+    el_s, ks_s = timed(lambda: gmm.scatter(x0s, resp0, mu), args.steps, args.warmup)
     te, ts = float(np.mean(ks_e)) / 1e3, float(np.mean(ks_s)) / 1e3
+    if world > 1:  # max over ranks of every per-step time
+        tk = float(np.mean(ks_k)) / 1e3
+        t = torch.tensor([tg, tr, te, ts, tk], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tg, tr, te, ts, tk = t.tolist()
+        dist.barrier()
+        if rank != 0:
+            dist.destroy_process_group()
+            return
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         S = 4000
         xs = x0[:S].cpu().numpy()
         t0 = time.time()
@@ -196,18 +231,26 @@ def c4(args):
         cpu["gmm_em_iteration_sample"] = (
             "sklearn GaussianMixture E+M step (community_embeddings.py:27's estimator) on %d "
             "rows: %.2fs -> %.1f s per full-size iteration" % (S2, sel, sel * V / S2))
+    dist_cfg = {}
+    if world > 1:
+        dist_cfg = {"community_kernel_only_ms": tk * 1e3,
+                    "community_exchange": "all_gather_into_tensor of %d x %d fp32 rows (%s)" % (
+                        V, d, args.dist_backend),
+                    "em_exchange": "all-reduce of K + K d then K d^2 float64 statistics",
+                    "parallelism": "row shard x%d, replicated tables" % world}
     print(json.dumps({
         "metric": "community gradient + GMM responsibilities, 1M nodes K=50 d=128",
-        "value": flops / tg / 1e12, "unit": "TFLOP/s (community gradient pass)", "n_gpus": 1,
+        "value": flops / tg / 1e12, "unit": "TFLOP/s (community gradient pass)", "n_gpus": world,
+        "scaling": "strong",
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": tg * 1e3,
         "higher_is_better": True, "dtype": "f32", "data": "synthetic N(0,1) rows, random SPD",
         "config": {"workload": "configs[3]/C4: V=%d K=%d d=%d" % (V, K, d),
                    "gmm_resp_ms": tr * 1e3, "gmm_resp_tflops": flops / tr / 1e12,
                    "gmm_scatter_ms": ts * 1e3, "gmm_scatter_tflops": flops / ts / 1e12,
-                   "gmm_em_iteration_ms": te * 1e3},
-        "roofline": {"bound": "mfma", "achieved": flops / tg / 1e12,
-                     "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": flops / tg / 1e12 / F32_MFMA_PEAK_TFLOPS,
+                   "gmm_em_iteration_ms": te * 1e3, **dist_cfg},
+        "roofline": {"bound": "mfma", "achieved": flops / tg / 1e12 / world,
+                     "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (per GPU)",
+                     "frac": flops / tg / 1e12 / world / F32_MFMA_PEAK_TFLOPS,
                      "flops_per_pass": flops, "avg_kernel_ms": tg * 1e3},
         "cpu_baseline": cpu}))
 
@@ -273,6 +316,10 @@ def main():
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="c4 with N > 1: nccl (= RCCL); gloo only to rehearse on one GPU")
+    ap.add_argument("--all-ranks-device0", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (needs --dist-backend gloo)")
     ap.add_argument("--opt", action="append", default=[],
                     help="come_set_option knob, e.g. --opt o1_pipe=0 (A/B experiments)")
     args = ap.parse_args()

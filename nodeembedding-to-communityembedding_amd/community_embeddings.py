@@ -13,6 +13,14 @@
     (come_community_grad).  Every row's gradient depends only on that row (:65 snapshot), so rows
     outside ``nodes`` are left untouched by gathering/scattering the selected rows.
   * ``responsibilities(model)``: predict_proba of the fitted mixture on the current embedding.
+
+Multi-GPU (``distributed=True``): every rank holds a full replica of
+node_embedding (as after the SGNS phase) and owns the contiguous row block
+``shard_range(V, rank, N)``.  ``fit`` runs the GMM EM over the ranks' blocks with all-reduced
+sufficient statistics (come_amd.gmm, distributed=True) and all-gathers the responsibilities;
+``train`` applies the community gradient to the rank's block only (rows are independent, :65) and
+all-gathers the updated rows once per call (after all ``iter`` steps), so the replicas agree
+bit for bit with a single-GPU run.  No other exchange is needed.
 """
 import logging as log
 
@@ -20,6 +28,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check, ptr, stream_handle
+from .distributed import all_gather_rows, shard_range, world_of
 
 
 def gmm_resp(x, prec_chol, mu_prec, log_norm):
@@ -59,26 +68,38 @@ def community_grad(x, pi, mu, inv_cov, beta, lr, iters):
 
 
 class Community2Vec(object):
-    def __init__(self, model, lr, reg_covar=0, gmm_backend="gpu"):
+    def __init__(self, model, lr, reg_covar=0, gmm_backend="gpu", distributed=False,
+                 group=None):
         self.lr = lr
         self.gmm_backend = gmm_backend
+        self.distributed = bool(distributed)
+        self.group = group
         if gmm_backend == "gpu":
             from .gmm import GaussianMixture
             self.g_mixture = GaussianMixture(n_components=model.k, reg_covar=reg_covar,
-                                             covariance_type='full', n_init=10)
+                                             covariance_type='full', n_init=10,
+                                             distributed=distributed, group=group)
         elif gmm_backend == "sklearn":
+            if distributed:
+                raise ValueError("distributed=True needs gmm_backend='gpu'")
             from sklearn import mixture
             self.g_mixture = mixture.GaussianMixture(n_components=model.k, reg_covar=reg_covar,
                                                      covariance_type='full', n_init=10)
         else:
             raise ValueError("gmm_backend must be 'gpu' or 'sklearn'")
 
+    def _shard(self, V):
+        """(lo, hi) rows this rank owns ((0, V) on one process)."""
+        rank, world = world_of(self.group) if self.distributed else (0, 1)
+        return shard_range(V, rank, world)
+
     def fit(self, model):
         import torch
         log.info("Fitting: {} communities".format(model.k))
         dev = model.node_embedding.device
         if self.gmm_backend == "gpu":
-            self.g_mixture.fit(model.node_embedding)
+            lo, hi = self._shard(model.node_embedding.shape[0])
+            self.g_mixture.fit(model.node_embedding[lo:hi])
         else:
             self.g_mixture.fit(model.node_embedding.detach().cpu().numpy())
         cov32 = torch.from_numpy(self.g_mixture.covariances_.astype(np.float32)).to(dev)
@@ -88,10 +109,17 @@ class Community2Vec(object):
         model.pi = self.responsibilities(model)
 
     def responsibilities(self, model):
+        import torch
         g = self.g_mixture
-        pc, mp, ln = gmm_resp_params(g.weights_, g.means_, g.precisions_cholesky_,
-                                     model.node_embedding.device)
-        return gmm_resp(model.node_embedding, pc, mp, ln)
+        x = model.node_embedding
+        pc, mp, ln = gmm_resp_params(g.weights_, g.means_, g.precisions_cholesky_, x.device)
+        if not self.distributed:
+            return gmm_resp(x, pc, mp, ln)
+        V = x.shape[0]
+        lo, hi = self._shard(V)
+        pi = torch.empty((V, pc.shape[0]), dtype=torch.float32, device=x.device)
+        pi[lo:hi] = gmm_resp(x[lo:hi], pc, mp, ln)
+        return all_gather_rows(pi, self.group)
 
     def train(self, nodes, model, beta, chunksize=150, iter=1):
         import torch
@@ -99,11 +127,21 @@ class Community2Vec(object):
         rows = rows[rows >= 0]
         x = model.node_embedding
         if len(rows) == model.vocab_size and (np.sort(rows) == np.arange(len(rows))).all():
-            community_grad(x, model.pi, model.centroid, model.inv_covariance_mat, beta, self.lr,
-                           iter)
+            lo, hi = self._shard(x.shape[0])
+            if hi > lo:  # a row block of a C-contiguous table is itself contiguous
+                community_grad(x[lo:hi], model.pi[lo:hi], model.centroid,
+                               model.inv_covariance_mat, beta, self.lr, iter)
+            if self.distributed:
+                all_gather_rows(x, self.group)
             return
-        idx = torch.from_numpy(np.unique(rows)).to(x.device)
+        uniq = np.unique(rows)
+        idx = torch.from_numpy(uniq).to(x.device)
         sub = x.index_select(0, idx).contiguous()
-        community_grad(sub, model.pi.index_select(0, idx).contiguous(), model.centroid,
-                       model.inv_covariance_mat, beta, self.lr, iter)
+        lo, hi = self._shard(len(uniq))
+        if hi > lo:
+            part = sub[lo:hi]
+            community_grad(part, model.pi.index_select(0, idx[lo:hi]).contiguous(),
+                           model.centroid, model.inv_covariance_mat, beta, self.lr, iter)
+        if self.distributed:
+            all_gather_rows(sub, self.group)
         x.index_copy_(0, idx, sub)

@@ -1,4 +1,5 @@
-"""Multi-GPU data parallelism for the SGNS path: walk sharding + periodic delta all-reduce.
+"""Multi-GPU data parallelism: walk sharding + periodic delta all-reduce for the SGNS path, row
+sharding + all-gather / sufficient-statistics all-reduce for the community step and GMM EM.
 
 The reference is one process with Hogwild threads over shared numpy tables; it has
 no communication backend.  Across the GPUs of a node the same idea becomes: every rank (one
@@ -41,6 +42,54 @@ def shard_walks(walks, seeds, rank, world):
     """This rank's contiguous shard of (walks, seeds)."""
     lo, hi = shard_range(len(seeds), rank, world)
     return walks[lo:hi], seeds[lo:hi]
+
+
+def world_of(group=None):
+    """(rank, world) of this process in `group`; (0, 1) without torch.distributed."""
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def all_gather_rows(x, group=None):
+    """Row-sharded exchange for the community step: rank r owns rows
+    shard_range(V, r, N) of the replicated [V, ...] tensor x and has updated only those; afterwards
+    every replica holds every rank's rows.  One all_gather_into_tensor over shards padded to
+    ceil(V / N) rows (RCCL on the GPU, gloo in the CPU tests)."""
+    import torch.distributed as dist
+    rank, world = world_of(group)
+    if world == 1:
+        return x
+    V = x.shape[0]
+    chunk = -(-V // world)
+    lo, hi = shard_range(V, rank, world)
+    send = x.new_empty((chunk,) + tuple(x.shape[1:]))
+    send[:hi - lo].copy_(x[lo:hi])
+    recv = x.new_empty((world * chunk,) + tuple(x.shape[1:]))
+    dist.all_gather_into_tensor(recv, send, group=group)
+    for r in range(world):
+        if r != rank:
+            l, h = shard_range(V, r, world)
+            x[l:h].copy_(recv[r * chunk:r * chunk + (h - l)])
+    return x
+
+
+def all_reduce_sum(tensors, group=None):
+    """In-place SUM all-reduce of a list of same-dtype tensors as ONE flat collective (the GMM
+    sufficient statistics: K + K d floats, then K d^2; few large calls suit xGMI rings)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = world_of(group)
+    if world == 1:
+        return tensors
+    flat = torch.cat([t.reshape(-1) for t in tensors])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    o = 0
+    for t in tensors:
+        t.copy_(flat[o:o + t.numel()].view_as(t))
+        o += t.numel()
+    return tensors
 
 
 def _fused(t):

@@ -21,6 +21,14 @@ Parity: with fixed initial parameters the iterations match sklearn's within fp32
 (tests/test_gpu_gmm.py).  The default k-means initialisation (k-means++ seeding then Lloyd,
 sklearn's KMeans(n_init=1) semantics) draws from its own device generator, so -- like the
 reference, whose GaussianMixture is unseeded -- which local optimum a fit reaches is not pinned.
+
+Multi-GPU (``distributed=True``): every rank passes ITS shard of the rows to
+``fit``; the E-step stays local and the M-step all-reduces the sufficient statistics over the
+process group -- nk and resp^T X (K + K d floats, float64) before the means, then the scatter
+matrices (K d^2) -- so every rank holds the same parameters after every iteration, equal to a
+single-process fit over the concatenated rows up to the summation order.  The lower bound is an
+all-reduced sum, so all ranks take the same convergence decision.  k-means init: k-means++ seeding
+on rank 0's shard, centres broadcast, Lloyd iterations with all-reduced centre sums and counts.
 """
 import math
 
@@ -28,6 +36,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check, ptr, stream_handle
+from .distributed import all_reduce_sum, world_of
 
 
 def _as_device_x(X, device=None):
@@ -80,7 +89,7 @@ class GaussianMixture(object):
     def __init__(self, n_components=1, covariance_type='full', tol=1e-3, reg_covar=1e-6,
                  max_iter=100, n_init=1, init_params='kmeans', weights_init=None,
                  means_init=None, precisions_init=None, random_state=None, kmeans_max_iter=300,
-                 kmeans_tol=1e-4, device=None):
+                 kmeans_tol=1e-4, device=None, distributed=False, group=None):
         if covariance_type != 'full':
             raise NotImplementedError("only covariance_type='full' (the reference's) is "
                                       "implemented")
@@ -100,18 +109,42 @@ class GaussianMixture(object):
         self.kmeans_max_iter = int(kmeans_max_iter)
         self.kmeans_tol = float(kmeans_tol)
         self.device = device
+        self.distributed = bool(distributed)
+        self.group = group
+
+    def _rank_world(self):
+        return world_of(self.group) if self.distributed else (0, 1)
+
+    def _prepare_x(self, X):
+        return _as_device_x(X, self.device)
+
+    def _global_sum(self, value, device):
+        """float64 scalar summed over the ranks (the value itself on one process)."""
+        import torch
+        if self._rank_world()[1] == 1:
+            return float(value)
+        t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+        all_reduce_sum([t], self.group)
+        return float(t[0])
 
     # ---- parameters -------------------------------------------------------------------------
     def _m_step(self, X, resp):
         """sklearn _estimate_gaussian_parameters (full): nk, means, covariances (+ reg)."""
         import torch
         V, d = X.shape
-        nk = resp.sum(0, dtype=torch.float64) + 10 * np.finfo(np.float64).eps
-        means = (resp.t() @ X).double() / nk[:, None]
-        S = scatter(X, resp, means.float())
-        cov = S.double() / nk[:, None, None]
+        world = self._rank_world()[1]
+        nk = resp.sum(0, dtype=torch.float64)
+        sx = (resp.t() @ X).double()
+        if world > 1:
+            all_reduce_sum([nk, sx], self.group)
+        nk = nk + 10 * np.finfo(np.float64).eps
+        means = sx / nk[:, None]
+        S = scatter(X, resp, means.float()).double()
+        if world > 1:
+            all_reduce_sum([S], self.group)
+        cov = S / nk[:, None, None]
         cov += self.reg_covar * torch.eye(d, dtype=torch.float64, device=X.device)
-        return nk / V, means, cov
+        return nk / (self._n_total if world > 1 else V), means, cov
 
     def _set_params(self, weights, means, cov):
         import torch
@@ -154,6 +187,11 @@ class GaussianMixture(object):
             seed = int(rs)
         else:
             seed = int(rs.randint(0, 2 ** 31 - 1))
+        if self._rank_world()[1] > 1:  # one stream for the job: rank 0's seed
+            import torch.distributed as dist
+            t = torch.tensor([seed], dtype=torch.int64, device=device)
+            dist.broadcast(t, 0, group=self.group)
+            seed = int(t[0])
         g.manual_seed(seed)
         return g
 
@@ -164,7 +202,46 @@ class GaussianMixture(object):
         import torch
         V, d = X.shape
         K = self.n_components
+        rank, world = self._rank_world()
         xx = (X * X).sum(1)
+        if rank == 0:
+            C = self._kmeans_plusplus(X, xx, gen)
+        else:
+            C = torch.empty((K, d), dtype=torch.float32, device=X.device)
+        if world > 1:
+            import torch.distributed as dist
+            dist.broadcast(C, 0, group=self.group)
+            s1 = X.sum(0, dtype=torch.float64)
+            s2 = (X.double() ** 2).sum(0)
+            all_reduce_sum([s1, s2], self.group)
+            n = float(self._n_total)
+            tol = self.kmeans_tol * float(((s2 - s1 * s1 / n) / (n - 1)).mean())
+        else:
+            tol = self.kmeans_tol * float(X.var(0).mean())
+        labels = None
+        for _ in range(self.kmeans_max_iter):
+            dist_ = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]
+            labels = torch.argmin(dist_, 1)
+            cnt = torch.bincount(labels, minlength=K).float()
+            S = torch.zeros((K, d), dtype=torch.float32, device=X.device)
+            S.index_add_(0, labels, X)
+            if world > 1:
+                all_reduce_sum([cnt, S], self.group)
+            newC = torch.where(cnt[:, None] > 0, S / cnt.clamp_min(1)[:, None], C)
+            shift = float(((newC - C) ** 2).sum())
+            C = newC
+            if shift <= tol:
+                break
+        dist_ = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]
+        return torch.argmin(dist_, 1)
+
+    def _kmeans_plusplus(self, X, xx, gen):
+        """sklearn's greedy k-means++ seeding on the rows X: [K, d] centres."""
+        import torch
+        V, d = X.shape
+        K = self.n_components
+        if V < K:
+            raise ValueError("k-means++ seeding needs >= n_components rows on rank 0")
         trials = 2 + int(math.log(K))
         first = torch.randint(0, V, (1,), generator=gen, device=X.device)
         centers = [X[first[0]]]
@@ -180,22 +257,7 @@ class GaussianMixture(object):
             best = int(torch.argmin(pots))
             closest, pot = dist[:, best].contiguous(), pots[best]
             centers.append(C[best])
-        C = torch.stack(centers)
-        tol = self.kmeans_tol * float(X.var(0).mean())
-        labels = None
-        for _ in range(self.kmeans_max_iter):
-            dist = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]
-            labels = torch.argmin(dist, 1)
-            cnt = torch.bincount(labels, minlength=K).float()
-            S = torch.zeros((K, d), dtype=torch.float32, device=X.device)
-            S.index_add_(0, labels, X)
-            newC = torch.where(cnt[:, None] > 0, S / cnt.clamp_min(1)[:, None], C)
-            shift = float(((newC - C) ** 2).sum())
-            C = newC
-            if shift <= tol:
-                break
-        dist = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]
-        return torch.argmin(dist, 1)
+        return torch.stack(centers)
 
     def _initialize(self, X, gen):
         import torch
@@ -227,11 +289,12 @@ class GaussianMixture(object):
 
     def fit_predict(self, X, y=None):
         import torch
-        X = _as_device_x(X, self.device)
+        X = self._prepare_x(X)
         V, d = X.shape
-        if V < self.n_components:
+        self._n_total = int(round(self._global_sum(V, X.device)))
+        if self._n_total < self.n_components:
             raise ValueError("Expected n_samples >= n_components but got n_components = %d, "
-                             "n_samples = %d" % (self.n_components, V))
+                             "n_samples = %d" % (self.n_components, self._n_total))
         if d > 128 or self.n_components > (4096 if d in (64, 128) else 64):
             raise ValueError("GPU GaussianMixture supports d <= 128 and n_components <= 64 "
                              "(<= 4096 for d = 64, 128)")
@@ -247,7 +310,7 @@ class GaussianMixture(object):
                 resp, lse = estep(X, self._e_pc, self._e_mp, self._e_ln)
                 w, mu, cov = self._m_step(X, resp)
                 self._set_params(w, mu, cov)
-                lb = float(lse.double().mean())
+                lb = self._global_sum(lse.double().sum(), X.device) / self._n_total
                 if abs(lb - prev) < self.tol:
                     converged = True
                     break
@@ -272,7 +335,7 @@ class GaussianMixture(object):
 
     # ---- inference ----------------------------------------------------------------------------
     def predict_proba(self, X):
-        X = _as_device_x(X, self.device)
+        X = self._prepare_x(X)
         return estep(X, self._e_pc, self._e_mp, self._e_ln)[0]
 
     def predict(self, X):
@@ -280,5 +343,8 @@ class GaussianMixture(object):
         return torch.argmax(self.predict_proba(X), 1)
 
     def score(self, X, y=None):
-        X = _as_device_x(X, self.device)
-        return float(estep(X, self._e_pc, self._e_mp, self._e_ln)[1].double().mean())
+        """Mean log-likelihood over all rows (over every rank's shard when distributed)."""
+        X = self._prepare_x(X)
+        lse = estep(X, self._e_pc, self._e_mp, self._e_ln)[1]
+        n = self._global_sum(X.shape[0], X.device)
+        return self._global_sum(lse.double().sum(), X.device) / n
