@@ -230,11 +230,36 @@ __global__ void __launch_bounds__(256, 2) k_community_mfma(CommArgs a) {
 }
 
 // GMM responsibilities on MFMA (d in {64, 128}): for each component the tile computes
-// Y = X P_k (A = the rows in the A layout of k_community_mfma, B = P_k staged [j][c]: a half-
-// wave reads 32 consecutive floats, conflict-free without padding), then sum_c (Y - mu P_k)^2
-// per row: squares summed over the CT column tiles in registers, then over the 32 columns of a
-// half-wave with the DPP / permlane16 stages 0-4.  Per-component log-probabilities go to
-// resp_out itself (scratch, one row per lane group), the softmax over k finishes in place.
+// Y = X P_k (A = the rows, lane (r, h) supplying x[row r][j = 2q + h] at k-step q; B = P_k staged
+// [j][c]: a half-wave reads 32 consecutive floats, conflict-free without padding), then
+// sum_c (Y - mu P_k)^2 per row: squares summed over the CT column tiles in registers, then over the
+// 32 columns of a half-wave with the DPP / permlane16 stages 0-4.  Per-component log-probabilities
+// go to resp_out itself (scratch, one row per lane group), the softmax over k finishes in place.
+//
+// Triangular skip: sklearn's precisions_cholesky_ after an M-step is UPPER triangular
+// (solve_triangular(chol(cov), I, lower=True).T), so column tile ct only needs rows j <= 32 ct + 31
+// of P_k, i.e. k-steps q < 16 (ct + 1): 10 of the 16 32x32 blocks at d = 128 (0.625 of the MFMAs).
+// The workgroup checks while staging P_k whether any entry below the diagonal is non-zero (a lower
+// factor, e.g. sklearn's cholesky(precisions_init, lower=True)) and then runs the full loop.  The
+// skipped MFMAs would only add exact zeros, so both paths give identical results.
+template <int D, bool TRI>
+__device__ __forceinline__ void resp_mfma_component(
+    const float (&xa)[D / 2], const float *Ps, int h, int r,
+    __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
+    constexpr int S = D / 2;
+    constexpr int CT = D / 32;
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+        const float av = xa[q];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            if (TRI && q >= 16 * (ct + 1)) continue;
+            const float bv = Ps[(2 * q + h) * D + ct * 32 + r];
+            acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ct], 0, 0, 0);
+        }
+    }
+}
+
 template <int D>
 __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
     constexpr int S = D / 2;
@@ -243,35 +268,41 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *Ps = sm;          // [D][D]
     float *mps = Ps + D * D;  // [D]
+    int *lower_k = reinterpret_cast<int *>(mps + D);  // = k + 1 when P_k has a lower entry
     const int tid = threadIdx.x;
     const int wid = tid >> 6, lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
     const int64_t blk0 = (int64_t)blockIdx.x * 128;
     const int64_t myrow = blk0 + wid * 32 + r;
     const bool rowok = myrow < a.V;
+    if (tid == 0) *lower_k = 0;
     float xa[S];
 #pragma unroll
-    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + q + S * h] : 0.0f;
+    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + 2 * q + h] : 0.0f;
     for (int k = 0; k < a.K; ++k) {
         __syncthreads();
         const float4 *Pk = reinterpret_cast<const float4 *>(a.prec_chol + (int64_t)k * D * D);
-        for (int o = tid; o < D * D / 4; o += 256) reinterpret_cast<float4 *>(Ps)[o] = Pk[o];
+        bool lower_nz = false;
+        for (int o = tid; o < D * D / 4; o += 256) {
+            const float4 v = Pk[o];
+            reinterpret_cast<float4 *>(Ps)[o] = v;
+            const int j = (o * 4) / D, c = (o * 4) % D;  // row j, columns c .. c+3
+            lower_nz |= (j > c && v.x != 0.0f) | (j > c + 1 && v.y != 0.0f) |
+                        (j > c + 2 && v.z != 0.0f) | (j > c + 3 && v.w != 0.0f);
+        }
+        if (lower_nz) *lower_k = k + 1;  // same value from every writer; no reset needed
         if (tid < D) mps[tid] = a.mu_prec[k * D + tid];
         __syncthreads();
+        const bool full = *lower_k == k + 1;
         f32x16 acc[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-#pragma unroll
-        for (int q = 0; q < S; ++q) {
-            const float av = xa[q];
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const float bv = Ps[(q + S * h) * D + ct * 32 + r];
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ct], 0, 0, 0);
-            }
-        }
+        if (full)
+            resp_mfma_component<D, false>(xa, Ps, h, r, acc);
+        else
+            resp_mfma_component<D, true>(xa, Ps, h, r, acc);
         const float lnk = a.log_norm[k];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -329,10 +360,33 @@ struct CovArgs {
     int K;
 };
 
+// Symmetric output: only the CT (CT + 1) / 2 tiles with rt <= ct are accumulated (10 of 16 at
+// d = 128, 3 of 4 at d = 64), TPW per wavefront over kCovWaves<D> wavefronts, and each off-diagonal
+// tile is also stored transposed -- S_k comes out exactly symmetric.
 template <int D>
-__global__ void __launch_bounds__(256) k_gmm_cov_mfma(CovArgs a) {
-    constexpr int CT = D / 32;
-    constexpr int TPW = CT * CT / 4;  // 32x32 tiles per wavefront
+struct CovShape {
+    static constexpr int CT = D / 32;
+    static constexpr int NT = CT * (CT + 1) / 2;
+    static constexpr int TPW = D == 128 ? 2 : 1;
+    static constexpr int WAVES = NT / TPW;  // 5 (d = 128), 3 (d = 64)
+    static_assert(NT % TPW == 0, "tiles must split evenly over the wavefronts");
+};
+
+// tile t of the upper triangle (row-major over rt <= ct) -> (rt, ct)
+__device__ __forceinline__ void upper_tile(int t, int CT, int &rt, int &ct) {
+    rt = 0;
+    while (t >= CT - rt) {
+        t -= CT - rt;
+        ++rt;
+    }
+    ct = rt + t;
+}
+
+template <int D>
+__global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArgs a) {
+    constexpr int CT = CovShape<D>::CT;
+    constexpr int TPW = CovShape<D>::TPW;
+    constexpr int NTH = 64 * CovShape<D>::WAVES;
     constexpr int LD = D + 4;
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     __shared__ __attribute__((aligned(16))) float xs[kCovRB * LD];
@@ -344,6 +398,9 @@ __global__ void __launch_bounds__(256) k_gmm_cov_mfma(CovArgs a) {
     if (c1 > a.V) c1 = a.V;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
+    int rts[TPW], cts[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) upper_tile(wid * TPW + t, CT, rts[t], cts[t]);
     if (tid < D) mus[tid] = a.means[k * D + tid];
     f32x16 acc[TPW];
 #pragma unroll
@@ -352,7 +409,7 @@ __global__ void __launch_bounds__(256) k_gmm_cov_mfma(CovArgs a) {
         for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
     for (int64_t b = c0; b < c1; b += kCovRB) {
         __syncthreads();
-        for (int o = tid; o < kCovRB * D / 4; o += 256) {
+        for (int o = tid; o < kCovRB * D / 4; o += NTH) {
             const int s = (o * 4) / D, c = (o * 4) % D;
             const int64_t row = b + s;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -371,10 +428,8 @@ __global__ void __launch_bounds__(256) k_gmm_cov_mfma(CovArgs a) {
             const float w = ws[s0 + h];
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
-                const int tile = wid * TPW + t;
-                const int rt = tile / CT, ct = tile % CT;
-                const float av = w * row[rt * 32 + r];
-                const float bv = row[ct * 32 + r];
+                const float av = w * row[rts[t] * 32 + r];
+                const float bv = row[cts[t] * 32 + r];
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
             }
         }
@@ -382,12 +437,13 @@ __global__ void __launch_bounds__(256) k_gmm_cov_mfma(CovArgs a) {
     float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * D * D;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        const int tile = wid * TPW + t;
-        const int rt = tile / CT, ct = tile % CT;
+        const int rt = rts[t], ct = cts[t];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            out[i * D + ct * 32 + r] = acc[t][e];
+            const int j = ct * 32 + r;
+            out[(int64_t)i * D + j] = acc[t][e];
+            if (rt != ct) out[(int64_t)j * D + i] = acc[t][e];
         }
     }
 }
@@ -506,7 +562,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
     RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K};
     if (mfma) {
         const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(d * d + d);
+        const size_t lds = sizeof(float) * (size_t)(d * d + d + 1);
         void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_mfma<64> : k_gmm_resp_mfma<128>;
         static bool attr_m = false;
         if (!attr_m) {
@@ -551,7 +607,8 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
     void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu
                                   : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
-    hipLaunchKernelGGL(kern, dim3(K, used), dim3(256), 0, (hipStream_t)stream, a);
+    const int threads = !mfma ? 256 : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
+    hipLaunchKernelGGL(kern, dim3(K, used), dim3(threads), 0, (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;
     hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
