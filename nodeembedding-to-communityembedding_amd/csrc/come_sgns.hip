@@ -1,6 +1,10 @@
 // come_sgns.hip -- launchers and C-ABI entry points of the SGNS kernels (come_sgns_impl.h).
 #include <string.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "come_sgns_impl.h"
 
 namespace come {
@@ -26,6 +30,8 @@ static int g_opt_o2_pair_atomics = 0;  // 1 = HOG node rows: one atomic per pair
 static int g_opt_rows_per_wave = 16;     // O2
 static int g_opt_o1_rows_per_wave = 12;  // O1
 static int g_opt_max_waves = 0;
+static int g_opt_o1_blocks_per_cu = 0;    // O1 grid cap (0 = 6 four-wave workgroups per CU)
+static int g_opt_resident_cap = 0;        // 1 = clamp grids to resident workgroups (A/B)
 
 // Cap on the number of workgroups of a Hogwild launch (0 = none).
 static int64_t hog_max_blocks(int64_t V, int wpb, int rows_per_wave) {
@@ -48,8 +54,31 @@ static const KernelSet &kernel_set(int d, int *full) {
 }
 static int maxn_index(int n) { return n <= 5 ? 0 : (n <= 10 ? 1 : 2); }
 
+// Workgroups of `fn` resident per CU at this block size and LDS (cached; 0 = unknown).  Clamping a
+// grid-stride launch to it is an A/B knob only (resident_cap=1): measured on O1 at C2 (d = 128,
+// 7 waves/SIMD resident), 4-wave workgroups per CU 8 (over-subscribed) / 7 (clamped) / 6 / 5 / 4
+// -> 1.28 / 1.42 / 1.08 / 1.12 / 1.27 ms per pass (profiles/r01h_ab_o1_grid.txt): what matters
+// is the number of wavefronts contending for the memory system, 24 per CU as for O2.
+static int resident_blocks(void *fn, int threads, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<void *, int, size_t>, int> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto key = std::make_tuple(fn, threads, lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void *)fn, threads, lds) !=
+            hipSuccess || n < 0) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    cache[key] = n;
+    return n;
+}
+
 // Launch `fn` with one wavefront per unit (walk / edge), `wpb` wavefronts per workgroup, grid
-// capped at `blocks_per_cu` workgroups per CU (grid-stride beyond); SEQUENTIAL = one wavefront.
+// capped at `blocks_per_cu` workgroups per CU and at what is resident (grid-stride beyond);
+// SEQUENTIAL = one wavefront.
 static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int blocks_per_cu,
                   size_t lds_bytes, void *stream, int64_t max_blocks = 0) {
     int dev = 0;
@@ -61,6 +90,8 @@ static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int bl
         block = dim3(64);
     } else {
         int64_t blocks = (units + wpb - 1) / wpb;
+        const int res = resident_blocks(fn, 64 * wpb, lds_bytes);
+        if (res > 0 && blocks_per_cu > res && g_opt_resident_cap) blocks_per_cu = res;
         int64_t cap = (int64_t)num_cus(dev) * blocks_per_cu;
         if (max_blocks > 0 && max_blocks < cap) cap = max_blocks;
         if (blocks > cap) blocks = cap;
@@ -178,7 +209,8 @@ extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges,
     O1Args a{node, edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
-    return launch(ks.o1[full][maxn_index(negative)], &a, E, mode, 4, 8, 0, stream,
+    return launch(ks.o1[full][maxn_index(negative)], &a, E, mode, 4,
+                  g_opt_o1_blocks_per_cu > 0 ? g_opt_o1_blocks_per_cu : 6, 0, stream,
                   mode == COME_MODE_HOGWILD ? hog_max_blocks(V, 4, g_opt_o1_rows_per_wave) : 0);
 }
 
@@ -249,7 +281,9 @@ extern "C" int come_set_option(const char *name, int value) {
                 {"o2_pair_atomics", &g_opt_o2_pair_atomics},
                 {"rows_per_wave", &g_opt_rows_per_wave},
                 {"o1_rows_per_wave", &g_opt_o1_rows_per_wave},
-                {"max_waves", &g_opt_max_waves}};
+                {"max_waves", &g_opt_max_waves},
+                {"o1_blocks_per_cu", &g_opt_o1_blocks_per_cu},
+                {"resident_cap", &g_opt_resident_cap}};
     for (auto &o : opts)
         if (!strcmp(o.k, name)) {
             *o.v = value;

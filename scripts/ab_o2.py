@@ -46,7 +46,7 @@ def main():
     seeds = torch.from_numpy(tsi.draw_seeds(args.walks).view(np.int64)).to(dev)
     pairs = tsi.count_o2_pairs(walks.cpu().numpy(), 5)
     keys = ["o2_kernel", "o2_blocks_per_cu", "o2_plain_writeback", "o2_waves_per_block",
-            "o2_static", "o2_pair_atomics"]
+            "o2_static", "o2_pair_atomics", "resident_cap"]
     packed = tsi.pack_table(m.table)  # variant key "packed=1" draws from the packed table
     # warm the tables past the all-zero context rows, then time every launch from that state
     for _ in range(args.warm_launches):
