@@ -132,3 +132,24 @@ def test_community2vec_gpu_fit_sets_model_buffers():
     covm = m.covariance_mat.cpu().numpy()
     np.testing.assert_allclose(np.einsum("kij,kjl->kil", inv, covm),
                                np.broadcast_to(np.eye(64), covm.shape), atol=1e-3)
+
+
+def test_community2vec_distributed_flag_single_process_matches():
+    """distributed=True without an initialised process group is the single-GPU path: the row
+    shard is every row and no collective runs (tests/test_distributed_c4.py covers world 2)."""
+    from come_amd.community_embeddings import Community2Vec
+    from come_amd.model import Model
+    X, w, mu, cov = problem(2000, 3, 128, 5, sep=4.0)
+    outs = []
+    for distributed in (False, True):
+        np.random.seed(0)
+        m = Model((np.arange(1, 2001), np.ones(2000)), size=128, table_size=1000, k=3)
+        m.node_embedding.copy_(torch.as_tensor(X, device=m.node_embedding.device))
+        c = Community2Vec(m, lr=0.1, reg_covar=1e-5, distributed=distributed)
+        np.random.seed(1)
+        c.fit(m)
+        c.train(np.arange(1, 2001), m, beta=0.1, iter=2)
+        outs.append((m.pi.cpu().numpy(), m.node_embedding.cpu().numpy()))
+    # (k-means' index_add_ is atomic on the GPU, so fits agree to rounding, not bit for bit)
+    np.testing.assert_allclose(outs[0][0], outs[1][0], atol=1e-4)
+    np.testing.assert_allclose(outs[0][1], outs[1][1], atol=1e-4)
