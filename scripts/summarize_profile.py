@@ -10,6 +10,7 @@ Usage: python scripts/summarize_profile.py gpurun_out/prof_r01 r01
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -38,15 +39,18 @@ def main(src, tag, kernel=KERNEL):
     cfg = bench["config"]
     pairs = cfg["pairs_per_step_per_gpu"]
     alg = bench["roofline"]["bytes_per_pair"] * pairs
+    m = re.search(r"d=(\d+), negative=(\d+)", cfg["workload"])
+    dim, neg = int(m.group(1)), int(m.group(2))
     traffic = {"kernel": row["Name"], "tag": tag, "walks_per_launch": cfg["walks_per_step_per_gpu"],
-               "dim": 128, "negative": 5, "hbm_bytes_per_launch": read_b + write_b,
+               "dim": dim, "negative": neg, "hbm_bytes_per_launch": read_b + write_b,
                "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
                "algorithmic_bytes_per_launch": alg, "pairs_per_launch": pairs,
                "rocprof_avg_kernel_ms": avg_ms,
                "bench_event_avg_kernel_ms": bench["roofline"]["avg_kernel_ms"],
                "actual_hbm_GBps": (read_b + write_b) / avg_ms / 1e6,
                "raw": pmc}
-    json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    if cfg["workload"].startswith("configs[2]/C3"):  # the default bench line reads this one
+        json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     json.dump(traffic, open(os.path.join(dst, "%s_traffic.json" % tag), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
