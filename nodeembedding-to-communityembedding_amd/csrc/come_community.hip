@@ -99,6 +99,7 @@ struct RespArgs {
     int64_t V;
     int d;
     int K;
+    const int *lower;  // MFMA path: [K], 1 if prec_chol[k] has a non-zero below the diagonal
 };
 
 __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
@@ -263,24 +264,77 @@ __global__ void __launch_bounds__(256, 2) k_community_mfma(CommArgs a) {
 // Triangular skip: sklearn's precisions_cholesky_ after an M-step is UPPER triangular
 // (solve_triangular(chol(cov), I, lower=True).T), so column tile ct only needs rows j <= 32 ct + 31
 // of P_k, i.e. k-steps q < 16 (ct + 1): 10 of the 16 32x32 blocks at d = 128 (0.625 of the MFMAs).
-// The workgroup checks while staging P_k whether any entry below the diagonal is non-zero (a lower
-// factor, e.g. sklearn's cholesky(precisions_init, lower=True)) and then runs the full loop.  The
-// skipped MFMAs would only add exact zeros, so both paths give identical results.
-template <int D, bool TRI>
-__device__ __forceinline__ void resp_mfma_component(
-    const float (&xa)[D / 2], const float *Ps, int h, int r,
+// k_gmm_lower_flags marks the components with a non-zero below the diagonal (a lower factor, e.g.
+// sklearn's cholesky(precisions_init, lower=True)); those run the full loop.  The skipped MFMAs
+// would only add exact zeros, so both paths give identical results.
+//
+// Staging is asynchronous: the k-steps q < S/2 read only rows j < D/2 of P_k ("half A"), the
+// others rows >= D/2 ("half B").  After every wavefront has finished half A of component k
+// (barrier), half A of P_{k+1} is copied global -> LDS by global_load_lds_dwordx4 (1 KiB per wave
+// instruction, lane-linear = the unpadded row-major image) while the half-B MFMAs and the epilogue
+// of k run; half B and mu_{k+1} P_{k+1} follow after the next barrier, in flight during the next
+// half A.  Each barrier is a plain __syncthreads (its vmcnt(0) retires exactly the copies the next
+// phase reads).  No VGPRs are spent on staging.
+__global__ void __launch_bounds__(256) k_gmm_lower_flags(const float *__restrict__ P, int D,
+                                                         int *__restrict__ flags) {
+    const float *Pk = P + (int64_t)blockIdx.x * D * D;
+    int nz = 0;
+    for (int o = threadIdx.x; o < D * D; o += 256) nz |= (o / D > o % D) && Pk[o] != 0.0f;
+    nz = __syncthreads_or(nz);
+    if (threadIdx.x == 0) flags[blockIdx.x] = nz ? 1 : 0;
+}
+
+// One code path for both cases: the skippable MFMAs (a compile-time set after unrolling) are
+// guarded by the wave-uniform `full` flag; two unrolled copies pushed the kernel past 256 VGPRs.
+template <int D, int Q0, int Q1>
+__device__ __forceinline__ void resp_mfma_steps(
+    const float (&xa)[D / 2], const float *Ps, int h, int r, bool full,
     __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
-    constexpr int S = D / 2;
     constexpr int CT = D / 32;
 #pragma unroll
-    for (int q = 0; q < S; ++q) {
+    for (int q = Q0; q < Q1; ++q) {
         const float av = xa[q];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-            if (TRI && q >= 16 * (ct + 1)) continue;
+            if (q >= 16 * (ct + 1) && !full) continue;
             const float bv = Ps[(2 * q + h) * D + ct * 32 + r];
             acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ct], 0, 0, 0);
         }
+    }
+}
+
+// copy rows [half * D/2, half * D/2 + D/2) of P_k into the LDS image (wavefront wid of 4)
+template <int D>
+__device__ __forceinline__ void resp_stage_half(const float *Pk, float *sm, int half, int wid,
+                                                int lane) {
+    constexpr int PIECES = D * D / 2 / 256;  // 1 KiB wave instructions per half
+#pragma unroll
+    for (int i = wid; i < PIECES; i += 4) {
+        const int off = half * (D * D / 2) + i * 256;
+        __builtin_amdgcn_global_load_lds(Pk + off + lane * 4, sm + off, 16, 0, 0);
+    }
+}
+
+// mu_k P_k (D floats) into sm[D*D .. D*D + 256): wavefront 0, lanes past D/4 re-read the last
+// 16 B (their copies land in the unused tail of the 1 KiB region)
+template <int D>
+__device__ __forceinline__ void resp_stage_mp(const float *mp, float *sm, int wid, int lane) {
+    if (wid == 0) {
+        const int src = lane * 4 < D ? lane * 4 : D - 4;
+        __builtin_amdgcn_global_load_lds(mp + src, sm + D * D, 16, 0, 0);
+    }
+}
+
+// lower[k] and log_norm[k] into sm[D*D + 256 ..]: lanes 0 and 1 of wavefront 0 (a vector load of
+// them would make the compiler wait vmcnt(0) at their first use -- draining the copies in flight;
+// loaded from LDS after the barrier instead)
+template <int D>
+__device__ __forceinline__ void resp_stage_params(const RespArgs &a, int k, float *sm, int wid,
+                                                  int lane) {
+    if (wid == 0) {
+        const float *src = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
+                                     : a.log_norm + k;
+        __builtin_amdgcn_global_load_lds(src, sm + D * D + 256, 4, 0, 0);
     }
 }
 
@@ -290,44 +344,42 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
     constexpr int CT = D / 32;
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *Ps = sm;          // [D][D]
-    float *mps = Ps + D * D;  // [D]
-    int *lower_k = reinterpret_cast<int *>(mps + D);  // = k + 1 when P_k has a lower entry
+    const float *Ps = sm;          // [D][D]
+    const float *mps = sm + D * D;  // [D] (+ tail up to 256), then 64 floats of params
     const int tid = threadIdx.x;
-    const int wid = tid >> 6, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
     const int64_t blk0 = (int64_t)blockIdx.x * 128;
     const int64_t myrow = blk0 + wid * 32 + r;
     const bool rowok = myrow < a.V;
-    if (tid == 0) *lower_k = 0;
     float xa[S];
 #pragma unroll
     for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + 2 * q + h] : 0.0f;
+    resp_stage_half<D>(a.prec_chol, sm, 0, wid, lane);
+    resp_stage_half<D>(a.prec_chol, sm, 1, wid, lane);
+    resp_stage_mp<D>(a.mu_prec, sm, wid, lane);
+    resp_stage_params<D>(a, 0, sm, wid, lane);
+    __syncthreads();
     for (int k = 0; k < a.K; ++k) {
-        __syncthreads();
-        const float4 *Pk = reinterpret_cast<const float4 *>(a.prec_chol + (int64_t)k * D * D);
-        bool lower_nz = false;
-        for (int o = tid; o < D * D / 4; o += 256) {
-            const float4 v = Pk[o];
-            reinterpret_cast<float4 *>(Ps)[o] = v;
-            const int j = (o * 4) / D, c = (o * 4) % D;  // row j, columns c .. c+3
-            lower_nz |= (j > c && v.x != 0.0f) | (j > c + 1 && v.y != 0.0f) |
-                        (j > c + 2 && v.z != 0.0f) | (j > c + 3 && v.w != 0.0f);
-        }
-        if (lower_nz) *lower_k = k + 1;  // same value from every writer; no reset needed
-        if (tid < D) mps[tid] = a.mu_prec[k * D + tid];
-        __syncthreads();
-        const bool full = *lower_k == k + 1;
+        const float *pr = sm + D * D + 256;
+        const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(pr[0])) != 0;
+        const float lnk = pr[1];
+        const float *Pn = a.prec_chol + (int64_t)(k + 1) * D * D;
         f32x16 acc[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-        if (full)
-            resp_mfma_component<D, false>(xa, Ps, h, r, acc);
-        else
-            resp_mfma_component<D, true>(xa, Ps, h, r, acc);
-        const float lnk = a.log_norm[k];
+        resp_mfma_steps<D, 0, S / 2>(xa, Ps, h, r, full, acc);
+        // the copies issued before the loop back-edge are not tracked by the compiler's barrier
+        // fence (it emitted no vmcnt wait here): retire them explicitly before the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // half A of P_k and the params free; half B and mu_k P_k in LDS
+        if (k + 1 < a.K) {
+            resp_stage_half<D>(Pn, sm, 0, wid, lane);
+            resp_stage_params<D>(a, k + 1, sm, wid, lane);
+        }
+        resp_mfma_steps<D, S / 2, S>(xa, Ps, h, r, full, acc);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             float sq = 0.0f;
@@ -344,6 +396,12 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
             const int64_t row = blk0 + wid * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
             if (r == 0 && row < a.V) a.resp[row * a.K + k] = lnk - 0.5f * sq;
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // half B of P_k and mu_k P_k free; half A of P_{k+1} in LDS
+        if (k + 1 < a.K) {
+            resp_stage_half<D>(Pn, sm, 1, wid, lane);
+            resp_stage_mp<D>(a.mu_prec + (int64_t)(k + 1) * D, sm, wid, lane);
+        }
     }
     __threadfence_block();
     __syncthreads();
@@ -358,7 +416,6 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
         if (a.lse) a.lse[blk0 + tid] = lse;
     }
 }
-
 
 // ---- GMM M-step scatter matrices -------------------------------------------------------------
 //
@@ -573,7 +630,8 @@ extern "C" int come_gmm_resp(const float *x, int64_t V, int d, const float *prec
 extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol,
                               const float *mu_prec, const float *log_norm, int K, float *resp_out,
                               float *lse_out, void *stream) {
-    const bool mfma = (d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0;
+    const bool mfma = (d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0 &&
+                      ((uintptr_t)mu_prec % 16) == 0;
     if (V < 0 || d < 1 || d > 128 || K < 1 || K > 4096 || (!mfma && K > 64))
         return set_error(COME_E_INVALID, "gmm_resp: need V>=0, 1<=d<=128, 1<=K<=64 (K<=4096 "
                                          "for d = 64, 128)");
@@ -583,10 +641,17 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
     int dev;
     int rc = ensure_init(&dev);
     if (rc) return rc;
-    RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K};
+    RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K, nullptr};
     if (mfma) {
+        int *flags = (int *)stream_scratch(dev, stream, kScratchGmmFlags, sizeof(int) * K);
+        if (!flags) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+        hipLaunchKernelGGL(k_gmm_lower_flags, dim3(K), dim3(256), 0, (hipStream_t)stream,
+                           prec_chol, d, flags);
+        rc = hip_error(hipGetLastError(), "k_gmm_lower_flags launch");
+        if (rc) return rc;
+        a.lower = flags;
         const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(d * d + d + 1);
+        const size_t lds = sizeof(float) * (size_t)(d * d + 320);
         void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_mfma<64> : k_gmm_resp_mfma<128>;
         static bool attr_m = false;
         if (!attr_m) {

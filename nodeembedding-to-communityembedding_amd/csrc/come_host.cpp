@@ -67,19 +67,24 @@ int ensure_init(int *device_out) {
 
 int num_cus(int device) { return g_cus[device] > 0 ? g_cus[device] : 256; }
 
-// Growable scratch for the O2 ring kernel's entry snapshots, one buffer per (device, stream) so
-// launches on different streams never share snapshot regions (never shrinks; growing frees the
-// old buffer, which waits for the device).
+// Growable scratch, one buffer per (device, slot, stream) so launches on different streams never
+// share a region (never shrinks; growing frees the old buffer, which waits for the device).
+// Slots: the O2 ring kernel's entry snapshots; the GMM E-step's per-component flags.
 struct Scratch {
     float *ptr = nullptr;
     size_t bytes = 0;
 };
-static std::unordered_map<void *, Scratch> g_scratch[kMaxDevices];
+static std::unordered_map<void *, Scratch> g_scratch[kMaxDevices][kScratchSlots];
 static std::mutex g_scratch_mu;
 
 float *o2_scratch(int device, void *stream, size_t bytes) {
+    return stream_scratch(device, stream, kScratchO2Snapshots, bytes);
+}
+
+float *stream_scratch(int device, void *stream, int slot, size_t bytes) {
+    if (slot < 0 || slot >= kScratchSlots) return nullptr;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    Scratch &s = g_scratch[device][stream];
+    Scratch &s = g_scratch[device][slot][stream];
     if (s.bytes >= bytes) return s.ptr;
     if (s.ptr) (void)hipFree(s.ptr);
     s = Scratch{};

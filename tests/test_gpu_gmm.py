@@ -60,6 +60,34 @@ def test_estep_vs_numpy(V, K, d):
     np.testing.assert_allclose(lse.cpu().numpy(), logsumexp(lp, 1), rtol=2e-5, atol=2e-3)
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_estep_mixed_factor_shapes(d):
+    """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
+    lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
+    loop.  Mixed in one launch, every component must match the float64 quadratic form."""
+    V, K = 1500, 6
+    rng = np.random.RandomState(d)
+    X = rng.standard_normal((V, d)).astype(np.float32)
+    mu = (rng.standard_normal((K, d)) * 0.3).astype(np.float32)
+    P = []
+    for k in range(K):
+        A = rng.standard_normal((d, d)) / np.sqrt(d)
+        kind = k % 3
+        P.append(np.triu(A) + 2 * np.eye(d) if kind == 0 else
+                 np.tril(A) + 2 * np.eye(d) if kind == 1 else A + 2 * np.eye(d))
+    P = np.stack(P)
+    ln = np.log(np.full(K, 1.0 / K))
+    mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
+    resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
+    Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
+    lp = ln[None] - 0.5 * (Y ** 2).sum(-1)
+    from scipy.special import logsumexp
+    ref_lse = logsumexp(lp, 1)
+    np.testing.assert_allclose(resp.cpu().numpy(), np.exp(lp - ref_lse[:, None]), atol=2e-4)
+    np.testing.assert_allclose(lse.cpu().numpy(), ref_lse, rtol=2e-5, atol=2e-3)
+
+
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
                                           (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None)])
 def test_scatter_vs_numpy(V, K, d, chunks):
