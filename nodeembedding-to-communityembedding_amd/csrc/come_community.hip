@@ -254,6 +254,172 @@ __global__ void __launch_bounds__(256, 2) k_community_mfma(CommArgs a) {
     }
 }
 
+// ---- community gradient with asynchronous staging (d in {64, 128}) ----------------------------
+//
+// Same contraction and operand roles as k_community_mfma, restructured so the staging of M_{k+1}
+// overlaps the MFMAs of M_k (the E-step recipe):
+//  * k-step q, half-wave h uses element j(q, h) = 8 (q/4) + 4 h + q%4: four consecutive k-steps of
+//    a lane read one 16-B group g = 2 (q/4) + h of row c = ct*32 + r of M_k (one ds_read_b128).
+//  * The groups split into set A (g < NG/2, k-steps q < S/2) and set B (the rest).  Each set is
+//    its own LDS image of D rows x RL = NG/2 groups, groups XOR-swizzled per row so that a 16-lane
+//    group of the b128 read (16 different rows, one logical group) hits 16 different 16-B bank
+//    slots.  A set image is lane-linear in 1 KiB pieces, so global_load_lds_dwordx4 fills it with
+//    the swizzle applied on the SOURCE address.
+//  * After the barrier ending set A of component k, set A of M_{k+1}, mu_{k+1} (double-buffered)
+//    and pi[:, k+1] for the block's rows are copied while set B computes; set B of M_{k+1} follows
+//    after the next barrier.  Explicit vmcnt(0) before each barrier.
+template <int D>
+struct CommAsync {
+    static constexpr int S = D / 2, CT = D / 32, NG = D / 4, RL = NG / 2;
+    static constexpr int RPB = 16 / RL;              // rows per 256-B bank row in a set image
+    static constexpr int SET = D * RL * 4;           // floats per set image (= D*D/2)
+    static constexpr int MUS = D * D;                // 2 x 256 floats: mu_k, double-buffered
+    static constexpr int PIS = D * D + 512;          // 128 floats: pi[row, k] of the block's rows
+    static constexpr int LDX = D + 4;                // epilogue row tile stride
+    static constexpr int LDS_FLOATS = (PIS + 128) > 128 * LDX ? (PIS + 128) : 128 * LDX;
+    __device__ static int swz(int c) { return (c / RPB) & (RL - 1); }
+    // float offset of logical group g of row c
+    __device__ static int at(int c, int g) {
+        const int set = g / RL, gp = g % RL;
+        return set * SET + c * RL * 4 + ((gp ^ swz(c)) * 4);
+    }
+    __device__ static void stage_set(const float *Mk, float *sm, int set, int wid, int lane) {
+        constexpr int PIECES = SET / 256;
+        constexpr int ROWS = 256 / (RL * 4);          // rows per 1 KiB piece
+#pragma unroll
+        for (int i = wid; i < PIECES; i += 4) {
+            const int c = i * ROWS + lane / RL, pg = lane % RL;
+            const int g = set * RL + (pg ^ swz(c));
+            __builtin_amdgcn_global_load_lds(Mk + c * D + g * 4, sm + set * SET + i * 256, 16, 0,
+                                             0);
+        }
+    }
+    __device__ static void stage_mu(const float *mu, float *sm, int buf, int wid, int lane) {
+        if (wid == 0) {
+            const int src = lane * 4 < D ? lane * 4 : D - 4;
+            __builtin_amdgcn_global_load_lds(mu + src, sm + MUS + buf * 256, 16, 0, 0);
+        }
+    }
+    __device__ static void stage_pi(const CommArgs &a, int64_t blk0, int k, float *sm, int wid,
+                                    int lane) {
+        if (wid < 2) {
+            int64_t row = blk0 + wid * 64 + lane;
+            if (row >= a.V) row = a.V - 1;
+            __builtin_amdgcn_global_load_lds(a.pi + row * a.K + k, sm + PIS + wid * 64, 4, 0, 0);
+        }
+    }
+};
+
+template <int D, int M0, int M1>
+__device__ __forceinline__ void community_async_steps(
+    const float (&xa)[D / 2], const float *sm, const float *mus, float p, int h, int r,
+    __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
+    using C = CommAsync<D>;
+    float4 bq[C::CT], bn[C::CT];
+    float4 mq, mn;
+#pragma unroll
+    for (int ct = 0; ct < C::CT; ++ct)
+        bq[ct] = *reinterpret_cast<const float4 *>(sm + C::at(ct * 32 + r, 2 * M0 + h));
+    mq = *reinterpret_cast<const float4 *>(mus + 8 * M0 + 4 * h);
+#pragma unroll
+    for (int m = M0; m < M1; ++m) {
+        if (m + 1 < M1) {
+#pragma unroll
+            for (int ct = 0; ct < C::CT; ++ct)
+                bn[ct] = *reinterpret_cast<const float4 *>(sm + C::at(ct * 32 + r, 2 * (m + 1) + h));
+            mn = *reinterpret_cast<const float4 *>(mus + 8 * (m + 1) + 4 * h);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float av = p * (xa[4 * m + i] - mq[i]);
+#pragma unroll
+            for (int ct = 0; ct < C::CT; ++ct)
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[ct][i], acc[ct], 0, 0, 0);
+        }
+        if (m + 1 < M1) {
+#pragma unroll
+            for (int ct = 0; ct < C::CT; ++ct) bq[ct] = bn[ct];
+            mq = mn;
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2) k_community_async(CommArgs a) {
+    using C = CommAsync<D>;
+    constexpr int S = C::S, CT = C::CT, LDX = C::LDX;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t blk0 = (int64_t)blockIdx.x * 128;
+    const int64_t myrow = blk0 + wid * 32 + r;
+    const bool rowok = myrow < a.V;
+    auto jcol = [&](int q) { return 8 * (q / 4) + 4 * h + (q % 4); };
+    float xa[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + jcol(q)] : 0.0f;
+
+    for (int it = 0; it < a.iters; ++it) {
+        __syncthreads();  // the previous epilogue's row tile is free
+        C::stage_set(a.inv_cov, sm, 0, wid, lane);
+        C::stage_set(a.inv_cov, sm, 1, wid, lane);
+        C::stage_mu(a.mu, sm, 0, wid, lane);
+        C::stage_pi(a, blk0, 0, sm, wid, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        f32x16 acc[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
+        for (int k = 0; k < a.K; ++k) {
+            const float p = sm[C::PIS + wid * 32 + r];
+            const float *mus = sm + C::MUS + (k & 1) * 256;
+            const float *Mn = a.inv_cov + (int64_t)(k + 1) * D * D;
+            community_async_steps<D, 0, S / 8>(xa, sm, mus, p, h, r, acc);  // set A of M_k
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // set A and pi free; set B of M_k in LDS
+            if (k + 1 < a.K) {
+                C::stage_set(Mn, sm, 0, wid, lane);
+                C::stage_mu(a.mu + (int64_t)(k + 1) * D, sm, (k + 1) & 1, wid, lane);
+                C::stage_pi(a, blk0, k + 1, sm, wid, lane);
+            }
+            community_async_steps<D, S / 8, S / 4>(xa, sm, mus, p, h, r, acc);  // set B of M_k
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // set B free; set A, mu and pi of k+1 in LDS
+            if (k + 1 < a.K) C::stage_set(Mn, sm, 1, wid, lane);
+        }
+        // epilogue: x -= lr * clip(coef * G, -5, 5), through a [128][LDX] LDS row tile (no copy
+        // is in flight: the last component issues none)
+        float *X = sm + wid * 32 * LDX;  // this wavefront's 32 rows
+#pragma unroll
+        for (int q = 0; q < S; ++q) X[r * LDX + jcol(q)] = xa[q];
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's rows are in LDS
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+                float *px = X + row * LDX + ct * 32 + r;
+                float g = acc[ct][e] * a.coef;
+                g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);
+                *px = *px - g * a.lr;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < S; ++q) xa[q] = X[r * LDX + jcol(q)];
+    }
+    if (rowok) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) a.x[myrow * D + jcol(q)] = xa[q];
+    }
+}
+
 // GMM responsibilities on MFMA (d in {64, 128}): for each component the tile computes
 // Y = X P_k (A = the rows, lane (r, h) supplying x[row r][j = 2q + h] at k-step q; B = P_k staged
 // [j][c]: a half-wave reads 32 consecutive floats, conflict-free without padding), then
@@ -581,6 +747,10 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float
 
 }  // namespace come
 
+namespace come {
+int g_comm_async = 1;  // come_set_option("community_async", 0): synchronous k_community_mfma
+}
+
 using namespace come;
 
 extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, const float *mu,
@@ -594,6 +764,23 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     int rc = ensure_init(&dev);
     if (rc) return rc;
     CommArgs a{x, pi, mu, inv_cov, V, d, K, (float)((double)beta / (double)K), lr, iters};
+    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 &&
+        ((uintptr_t)mu % 16) == 0 && g_comm_async) {
+        const unsigned grid = (unsigned)((V + 127) / 128);
+        const size_t lds = sizeof(float) * (size_t)(d == 64 ? CommAsync<64>::LDS_FLOATS
+                                                            : CommAsync<128>::LDS_FLOATS);
+        void (*kern)(CommArgs) = d == 64 ? k_community_async<64> : k_community_async<128>;
+        static bool attr_a = false;
+        if (!attr_a) {
+            (void)hipFuncSetAttribute((const void *)k_community_async<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void *)k_community_async<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_a = true;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
+        return hip_error(hipGetLastError(), "k_community_async launch");
+    }
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0) {
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(128 * (d + 4) + d);
