@@ -695,6 +695,94 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArg
     }
 }
 
+// Asynchronous form (A/B option "gmm_cov_async", off by default: 12.8 ms vs 11.5 ms at C4 -- the
+// 64 KiB double buffer halves the resident workgroups, profiles/r01h_ab_scatter_async.txt): the raw sample rows and their weights are copied global -> LDS by
+// global_load_lds_dwordx4 into a double buffer (64 rows x D, lane-linear 1 KiB pieces of the
+// unpadded image; a half-wave's reads of one row hit 32 consecutive banks), block b+1 in flight
+// while block b computes; the centring x - mu_k moves from the staging pass into the operand
+// reads (same fp32 subtraction, so the products are bit-identical to k_gmm_cov_mfma's).  Rows
+// past the chunk are clamped on the source side and get weight 0 at read time.
+template <int D>
+__global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovArgs a) {
+    constexpr int CT = CovShape<D>::CT;
+    constexpr int TPW = CovShape<D>::TPW;
+    constexpr int WAVES = CovShape<D>::WAVES;
+    constexpr int XB = kCovRB * D;       // floats per row buffer
+    constexpr int PIECES = XB / 256;     // 1 KiB pieces per row buffer
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    extern __shared__ __attribute__((aligned(16))) float smc[];  // [2][XB] rows, [2][64] weights
+    const int k = blockIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    int rts[TPW], cts[TPW];
+    float mr[TPW], mc[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        upper_tile(wid * TPW + t, CT, rts[t], cts[t]);
+        mr[t] = a.means[k * D + rts[t] * 32 + r];
+        mc[t] = a.means[k * D + cts[t] * 32 + r];
+    }
+    f32x16 acc[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+    auto stage = [&](int64_t b, int buf) {
+        for (int i = wid; i < PIECES; i += WAVES) {
+            const int f = i * 256 + lane * 4;    // float offset in the row buffer
+            int64_t row = b + f / D;
+            if (row >= c1) row = c1 - 1;
+            __builtin_amdgcn_global_load_lds(a.x + row * D + f % D, smc + buf * XB + i * 256, 16,
+                                             0, 0);
+        }
+        if (wid == WAVES - 1) {
+            int64_t row = b + lane;
+            if (row >= c1) row = c1 - 1;
+            __builtin_amdgcn_global_load_lds(a.resp + row * a.K + k, smc + 2 * XB + buf * 64, 4,
+                                             0, 0);
+        }
+    };
+    if (c0 < c1) stage(c0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int buf = 0;
+    for (int64_t b = c0; b < c1; b += kCovRB, buf ^= 1) {
+        if (b + kCovRB < c1) stage(b + kCovRB, buf ^ 1);
+        const float *xb = smc + buf * XB;
+        const float *wb = smc + 2 * XB + buf * 64;
+#pragma unroll 4
+        for (int s0 = 0; s0 < kCovRB; s0 += 2) {
+            const int sr = s0 + h;
+            const float *row = xb + sr * D;
+            const float w = b + sr < c1 ? wb[sr] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const float av = w * (row[rts[t] * 32 + r] - mr[t]);
+                const float bv = row[cts[t] * 32 + r] - mc[t];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // block b+1 landed; every wavefront is done with block b
+    }
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * D * D;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int rt = rts[t], ct = cts[t];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int j = ct * 32 + r;
+            out[(int64_t)i * D + j] = acc[t][e];
+            if (rt != ct) out[(int64_t)j * D + i] = acc[t][e];
+        }
+    }
+}
+
 // Any d <= 128 on the VALU: thread owns entries tid + 256 q of the d x d output.
 __global__ void __launch_bounds__(256) k_gmm_cov_valu(CovArgs a) {
     constexpr int MAXQ = 64;  // 128 * 128 / 256
@@ -749,6 +837,7 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float
 
 namespace come {
 int g_comm_async = 1;  // come_set_option("community_async", 0): synchronous k_community_mfma
+int g_cov_async = 0;   // come_set_option("gmm_cov_async", 1): k_gmm_cov_async (A/B; slower)
 }
 
 using namespace come;
@@ -881,10 +970,24 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const int used = V == 0 ? 1 : (int)((V + per - 1) / per);
     CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K};
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
-    void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu
-                                  : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
+    void (*kern)(CovArgs) =
+        !mfma ? k_gmm_cov_valu
+              : g_cov_async ? (d == 64 ? k_gmm_cov_async<64> : k_gmm_cov_async<128>)
+                            : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
     const int threads = !mfma ? 256 : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
-    hipLaunchKernelGGL(kern, dim3(K, used), dim3(threads), 0, (hipStream_t)stream, a);
+    size_t lds = 0;
+    if (mfma && g_cov_async) {
+        lds = sizeof(float) * (size_t)(2 * kCovRB * d + 2 * 64);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL(kern, dim3(K, used), dim3(threads), lds, (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;
     hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

@@ -31,6 +31,7 @@ float *o2_scratch(int device, void *stream, size_t bytes);
 constexpr int kScratchO2Snapshots = 0, kScratchGmmFlags = 1, kScratchSlots = 2;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
 extern int g_comm_async;  // community gradient kernel choice (come_set_option "community_async")
+extern int g_cov_async;   // GMM scatter kernel choice (come_set_option "gmm_cov_async")
 
 // Lemire fastmod: a % d for 32-bit a, d >= 1, from one 64-bit multiply-high.  m = 0 encodes
 // "d >= 2^32" (then a % d == a for every 32-bit a).
