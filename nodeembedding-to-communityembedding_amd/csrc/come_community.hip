@@ -697,8 +697,9 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArg
 
 // Asynchronous form (A/B option "gmm_cov_async", off by default: 12.8 ms vs 11.5 ms at C4 -- the
 // 64 KiB double buffer halves the resident workgroups, profiles/r01h_ab_scatter_async.txt): the
-// raw sample rows and their weights are copied global -> LDS by global_load_lds_dwordx4 into a double buffer (64 rows x D, lane-linear 1 KiB pieces of the
-// unpadded image; a half-wave's reads of one row hit 32 consecutive banks), block b+1 in flight
+// raw sample rows and their weights are copied global -> LDS by global_load_lds_dwordx4 into a
+// double buffer (64 rows x D, lane-linear 1 KiB pieces of the unpadded image; a half-wave's reads
+// of one row hit 32 consecutive banks), block b+1 in flight
 // while block b computes; the centring x - mu_k moves from the staging pass into the operand
 // reads (same fp32 subtraction, so the products are bit-identical to k_gmm_cov_mfma's).  Rows
 // past the chunk are clamped on the source side and get weight 0 at read time.
