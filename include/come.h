@@ -208,7 +208,7 @@ int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int
  * most V / rows_per_wave wavefronts in flight so updates stay sparse on small vocabularies;
  * defaults 16 / 12, 0 = no cap), "max_waves" (absolute cap on wavefronts in flight, 0 = none),
  * "o1_blocks_per_cu" (O1 grid cap in 4-wave workgroups per CU, 0 = 6), "resident_cap" (1 = also
- * clamp grids to the workgroups the occupancy API reports resident), "gmm_cov_async" (1 = k_gmm_cov_async, slower at C4), "community_async" (default 1:
+ * clamp grids to the workgroups the occupancy API reports resident), "gmm_cov_async" (default 1: k_gmm_cov_async; 0 = k_gmm_cov_mfma), "community_async" (default 1:
  * k_community_async; 0 = the synchronous-staging k_community_mfma).
  * Note: come_set_option() returns to the default only when set to the default value. */
 int come_set_option(const char *name, int value);

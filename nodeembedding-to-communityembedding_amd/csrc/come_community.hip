@@ -595,6 +595,7 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
 // chunks in a fixed order (deterministic, no float atomics).  blockIdx.x = k varies fastest, so
 // the K workgroups of one chunk run together and share its rows through L2 / MALL.
 constexpr int kCovRB = 64;
+constexpr int kCovAsyncRB = 32;  // k_gmm_cov_async: 2 x 16 KiB buffers keep 4 workgroups per CU
 
 struct CovArgs {
     const float *x;
@@ -695,8 +696,9 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArg
     }
 }
 
-// Asynchronous form (A/B option "gmm_cov_async", off by default: 12.8 ms vs 11.5 ms at C4 -- the
-// 64 KiB double buffer halves the resident workgroups, profiles/r01h_ab_scatter_async.txt): the
+// Asynchronous form (default; "gmm_cov_async" = 0 selects k_gmm_cov_mfma): 11.40 vs 11.54 ms at
+// C4 with 32-row blocks (2 x 16 KiB buffers keep 4 workgroups per CU; 64-row blocks halved the
+// resident workgroups and ran 12.8 ms; profiles/r01h_ab_scatter_async.txt).  The
 // raw sample rows and their weights are copied global -> LDS by global_load_lds_dwordx4 into a
 // double buffer (64 rows x D, lane-linear 1 KiB pieces of the unpadded image; a half-wave's reads
 // of one row hit 32 consecutive banks), block b+1 in flight
@@ -708,7 +710,7 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovAr
     constexpr int CT = CovShape<D>::CT;
     constexpr int TPW = CovShape<D>::TPW;
     constexpr int WAVES = CovShape<D>::WAVES;
-    constexpr int XB = kCovRB * D;       // floats per row buffer
+    constexpr int XB = kCovAsyncRB * D;  // floats per row buffer
     constexpr int PIECES = XB / 256;     // 1 KiB pieces per row buffer
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     extern __shared__ __attribute__((aligned(16))) float smc[];  // [2][XB] rows, [2][64] weights
@@ -751,12 +753,12 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovAr
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int buf = 0;
-    for (int64_t b = c0; b < c1; b += kCovRB, buf ^= 1) {
-        if (b + kCovRB < c1) stage(b + kCovRB, buf ^ 1);
+    for (int64_t b = c0; b < c1; b += kCovAsyncRB, buf ^= 1) {
+        if (b + kCovAsyncRB < c1) stage(b + kCovAsyncRB, buf ^ 1);
         const float *xb = smc + buf * XB;
         const float *wb = smc + 2 * XB + buf * 64;
 #pragma unroll 4
-        for (int s0 = 0; s0 < kCovRB; s0 += 2) {
+        for (int s0 = 0; s0 < kCovAsyncRB; s0 += 2) {
             const int sr = s0 + h;
             const float *row = xb + sr * D;
             const float w = b + sr < c1 ? wb[sr] : 0.0f;
@@ -838,7 +840,7 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float
 
 namespace come {
 int g_comm_async = 1;  // come_set_option("community_async", 0): synchronous k_community_mfma
-int g_cov_async = 0;   // come_set_option("gmm_cov_async", 1): k_gmm_cov_async (A/B; slower)
+int g_cov_async = 1;   // come_set_option("gmm_cov_async", 0): synchronous k_gmm_cov_mfma
 }
 
 using namespace come;
@@ -978,7 +980,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const int threads = !mfma ? 256 : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
     size_t lds = 0;
     if (mfma && g_cov_async) {
-        lds = sizeof(float) * (size_t)(2 * kCovRB * d + 2 * 64);
+        lds = sizeof(float) * (size_t)(2 * kCovAsyncRB * d + 2 * 64);
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<64>,

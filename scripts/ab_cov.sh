@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-for v in "" "--opt gmm_cov_async=0" "" "--opt gmm_cov_async=0"; do
+for v in "--opt gmm_cov_async=1" "" "--opt gmm_cov_async=1" ""; do
   timeout -k 10 200 python bench_aux.py --workload c4 --steps 20 --warmup 3 --no-cpu-baseline $v > gpurun_out/ab_c4.json 2>/dev/null || exit 1
   echo "variant [$v]: $(python -c "import json;d=json.load(open('gpurun_out/ab_c4.json'));c=d['config'];print(c['gmm_scatter_ms'], c['gmm_em_iteration_ms'])")"
 done
