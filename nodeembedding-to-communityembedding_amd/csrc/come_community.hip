@@ -596,6 +596,8 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
 // the K workgroups of one chunk run together and share its rows through L2 / MALL.
 constexpr int kCovRB = 64;
 constexpr int kCovAsyncRB = 32;  // k_gmm_cov_async: 2 x 16 KiB buffers keep 4 workgroups per CU
+constexpr int kCovKPB = 1;  // components per workgroup of k_gmm_cov_async (2 measured 13.4 ms vs
+                            // 11.4 ms at C4: profiles/r01h_ab_scatter_async.txt)
 
 struct CovArgs {
     const float *x;
@@ -705,16 +707,17 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArg
 // while block b computes; the centring x - mu_k moves from the staging pass into the operand
 // reads (same fp32 subtraction, so the products are bit-identical to k_gmm_cov_mfma's).  Rows
 // past the chunk are clamped on the source side and get weight 0 at read time.
-template <int D>
+template <int D, int KPB>
 __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovArgs a) {
     constexpr int CT = CovShape<D>::CT;
     constexpr int TPW = CovShape<D>::TPW;
     constexpr int WAVES = CovShape<D>::WAVES;
     constexpr int XB = kCovAsyncRB * D;  // floats per row buffer
     constexpr int PIECES = XB / 256;     // 1 KiB pieces per row buffer
+    static_assert(KPB * kCovAsyncRB <= 64, "one weight copy per block: KPB x rows <= 64 lanes");
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     extern __shared__ __attribute__((aligned(16))) float smc[];  // [2][XB] rows, [2][64] weights
-    const int k = blockIdx.x;
+    const int kb = blockIdx.x * KPB;  // components kb .. kb + KPB - 1 share the staged rows
     const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
     int64_t c1 = c0 + a.rows_per_chunk;
     if (c1 > a.V) c1 = a.V;
@@ -722,18 +725,24 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovAr
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
     int rts[TPW], cts[TPW];
-    float mr[TPW], mc[TPW];
+    float mr[KPB][TPW], mc[KPB][TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         upper_tile(wid * TPW + t, CT, rts[t], cts[t]);
-        mr[t] = a.means[k * D + rts[t] * 32 + r];
-        mc[t] = a.means[k * D + cts[t] * 32 + r];
+#pragma unroll
+        for (int j = 0; j < KPB; ++j) {
+            const int k = kb + j < a.K ? kb + j : a.K - 1;
+            mr[j][t] = a.means[k * D + rts[t] * 32 + r];
+            mc[j][t] = a.means[k * D + cts[t] * 32 + r];
+        }
     }
-    f32x16 acc[TPW];
+    f32x16 acc[KPB][TPW];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t)
+    for (int j = 0; j < KPB; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.0f;
     auto stage = [&](int64_t b, int buf) {
         for (int i = wid; i < PIECES; i += WAVES) {
             const int f = i * 256 + lane * 4;    // float offset in the row buffer
@@ -742,8 +751,10 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovAr
             __builtin_amdgcn_global_load_lds(a.x + row * D + f % D, smc + buf * XB + i * 256, 16,
                                              0, 0);
         }
-        if (wid == WAVES - 1) {
-            int64_t row = b + lane;
+        if (wid == WAVES - 1) {  // lane = j * 32 + s: weight of sample s for component kb + j
+            const int j = lane / kCovAsyncRB;
+            const int k = kb + j < a.K ? kb + j : a.K - 1;
+            int64_t row = b + lane % kCovAsyncRB;
             if (row >= c1) row = c1 - 1;
             __builtin_amdgcn_global_load_lds(a.resp + row * a.K + k, smc + 2 * XB + buf * 64, 4,
                                              0, 0);
@@ -761,27 +772,36 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovAr
         for (int s0 = 0; s0 < kCovAsyncRB; s0 += 2) {
             const int sr = s0 + h;
             const float *row = xb + sr * D;
-            const float w = b + sr < c1 ? wb[sr] : 0.0f;
+            const bool ok = b + sr < c1;
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
-                const float av = w * (row[rts[t] * 32 + r] - mr[t]);
-                const float bv = row[cts[t] * 32 + r] - mc[t];
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+                const float xr = row[rts[t] * 32 + r], xc = row[cts[t] * 32 + r];
+#pragma unroll
+                for (int j = 0; j < KPB; ++j) {
+                    const float w = ok ? wb[j * kCovAsyncRB + sr] : 0.0f;
+                    const float av = w * (xr - mr[j][t]);
+                    const float bv = xc - mc[j][t];
+                    acc[j][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j][t], 0, 0, 0);
+                }
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // block b+1 landed; every wavefront is done with block b
     }
-    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * D * D;
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        const int rt = rts[t], ct = cts[t];
+    for (int j = 0; j < KPB; ++j) {
+        if (kb + j >= a.K) break;
+        float *out = a.out + ((int64_t)blockIdx.y * a.K + kb + j) * D * D;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int j = ct * 32 + r;
-            out[(int64_t)i * D + j] = acc[t][e];
-            if (rt != ct) out[(int64_t)j * D + i] = acc[t][e];
+        for (int t = 0; t < TPW; ++t) {
+            const int rt = rts[t], ct = cts[t];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int jj = ct * 32 + r;
+                out[(int64_t)i * D + jj] = acc[j][t][e];
+                if (rt != ct) out[(int64_t)jj * D + i] = acc[j][t][e];
+            }
         }
     }
 }
@@ -975,7 +995,8 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
     void (*kern)(CovArgs) =
         !mfma ? k_gmm_cov_valu
-              : g_cov_async ? (d == 64 ? k_gmm_cov_async<64> : k_gmm_cov_async<128>)
+              : g_cov_async ? (d == 64 ? k_gmm_cov_async<64, kCovKPB>
+                                       : k_gmm_cov_async<128, kCovKPB>)
                             : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
     const int threads = !mfma ? 256 : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
     size_t lds = 0;
@@ -983,14 +1004,15 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
         lds = sizeof(float) * (size_t)(2 * kCovAsyncRB * d + 2 * 64);
         static bool attr = false;
         if (!attr) {
-            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<64>,
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<64, kCovKPB>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<128>,
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<128, kCovKPB>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr = true;
         }
     }
-    hipLaunchKernelGGL(kern, dim3(K, used), dim3(threads), lds, (hipStream_t)stream, a);
+    const unsigned gx = (mfma && g_cov_async) ? (unsigned)((K + kCovKPB - 1) / kCovKPB) : K;
+    hipLaunchKernelGGL(kern, dim3(gx, used), dim3(threads), lds, (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;
     hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
