@@ -25,7 +25,7 @@ def main():
         for opt in (0, 1):
             _lib.set_option("gmm_cov_async", opt)
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
-        _lib.set_option("gmm_cov_async", 0)
+        _lib.set_option("gmm_cov_async", 1)  # the default
         diff = float(np.abs(out[0] - out[1]).max())
         print("V=%d K=%d d=%d chunks=%s: max |async - sync| = %g" % (V, K, d, chunks, diff))
         bad += diff != 0.0

@@ -181,3 +181,24 @@ def test_community2vec_distributed_flag_single_process_matches():
     # (k-means' index_add_ is atomic on the GPU, so fits agree to rounding, not bit for bit)
     np.testing.assert_allclose(outs[0][0], outs[1][0], atol=1e-4)
     np.testing.assert_allclose(outs[0][1], outs[1][1], atol=1e-4)
+
+
+@pytest.mark.parametrize("V,K,d,chunks", [(4097, 5, 128, 7), (999, 3, 128, None),
+                                          (5000, 3, 64, None), (65, 4, 64, 2)])
+def test_scatter_async_matches_sync(V, K, d, chunks):
+    """k_gmm_cov_async (default) only moves the centring from the staging pass into the operand
+    reads of k_gmm_cov_mfma: the scatter matrices must be bit-identical."""
+    from come_amd import _lib
+    rng = np.random.RandomState(V + K + d)
+    t = lambda a: torch.as_tensor(a, device=dev())  # noqa: E731
+    x = t(rng.standard_normal((V, d)).astype(np.float32))
+    resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
+    mu = t(rng.standard_normal((K, d)).astype(np.float32))
+    out = []
+    try:
+        for opt in (0, 1):
+            _lib.set_option("gmm_cov_async", opt)
+            out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
+    finally:
+        _lib.set_option("gmm_cov_async", 1)
+    np.testing.assert_array_equal(out[0], out[1])
