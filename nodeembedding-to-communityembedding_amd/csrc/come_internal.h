@@ -30,6 +30,7 @@ int64_t *launch_counter(int device, void *stream);
 float *o2_scratch(int device, void *stream, size_t bytes);
 constexpr int kScratchO2Snapshots = 0, kScratchGmmFlags = 1, kScratchSlots = 2;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
+extern int g_walk_staged;  // walker output staging (come_set_option "walk_staged")
 extern int g_comm_async;  // community gradient kernel choice (come_set_option "community_async")
 extern int g_cov_async;   // GMM scatter kernel choice (come_set_option "gmm_cov_async")
 

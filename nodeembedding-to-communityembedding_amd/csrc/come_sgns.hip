@@ -285,7 +285,8 @@ extern "C" int come_set_option(const char *name, int value) {
                 {"o1_blocks_per_cu", &g_opt_o1_blocks_per_cu},
                 {"resident_cap", &g_opt_resident_cap},
                 {"community_async", &g_comm_async},
-                {"gmm_cov_async", &g_cov_async}};
+                {"gmm_cov_async", &g_cov_async},
+                {"walk_staged", &g_walk_staged}};
     for (auto &o : opts)
         if (!strcmp(o.k, name)) {
             *o.v = value;

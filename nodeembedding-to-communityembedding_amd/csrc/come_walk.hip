@@ -84,9 +84,64 @@ __global__ void __launch_bounds__(256) k_random_walks(WalkArgs a) {
     for (; t < a.L; ++t) row[t] = -1;
 }
 
+// The same walks (same Philox counters, same steps), with the output staged through LDS: a lane's
+// row is L ints at a 4L-byte stride, so the direct kernel's per-step store touches 64 cache lines
+// per wavefront.  Here each lane fills a WALK_CHUNK-step slice of its row in LDS and the
+// workgroup then writes the slice out as 64-B row segments, 16 lanes per segment.  Lanes past P
+// or past a dead end keep going through the chunk loop (they emit -1) so every lane reaches the
+// barriers.
+constexpr int WALK_BLOCK = 256;
+constexpr int WALK_CHUNK = 16;
+
+__global__ void __launch_bounds__(WALK_BLOCK) k_random_walks_staged(WalkArgs a) {
+    __shared__ int32_t tile[WALK_BLOCK][WALK_CHUNK + 1];  // +1: column writes hit distinct banks
+    const int tid = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * WALK_BLOCK;
+    const int64_t w = w0 + tid;
+    const uint64_t gw = (uint64_t)(a.walk_offset + w);
+    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+    int32_t start = -1;
+    if (w < a.P) start = a.starts[w];
+    bool alive = start >= 0 && start < a.V;  // not a node: an empty walk
+    int32_t cur = alive ? start : -1;
+    const int64_t rows = a.P - w0 < WALK_BLOCK ? a.P - w0 : WALK_BLOCK;
+    for (int c0 = 0; c0 < a.L; c0 += WALK_CHUNK) {
+        const int cn = a.L - c0 < WALK_CHUNK ? a.L - c0 : WALK_CHUNK;
+        for (int j = 0; j < cn; ++j) {
+            const int t = c0 + j;
+            if (alive && t > 0) {
+                const int64_t b = a.rowptr[cur];
+                const int64_t deg = a.rowptr[cur + 1] - b;
+                if (deg <= 0) {  // graph_utils.py:44-45
+                    alive = false;
+                } else {
+                    const Philox x = philox4x32_10((uint32_t)t, (uint32_t)gw, (uint32_t)(gw >> 32),
+                                                   0u, k0, k1);
+                    if ((x.r[1] >> 8) >= a.restart_threshold) {  // rand.random() >= alpha (:39)
+                        const uint32_t pick = (uint32_t)(((uint64_t)x.r[0] * (uint64_t)deg) >> 32);
+                        cur = a.col[b + pick];
+                    } else {
+                        cur = start;  // restart (:42)
+                    }
+                }
+            }
+            tile[tid][j] = alive ? (a.emit ? a.emit[cur] : cur) : -1;
+        }
+        __syncthreads();
+        // rows x cn slice -> global, consecutive lanes on consecutive columns of one row
+        for (int i = tid; i < (int)rows * cn; i += WALK_BLOCK) {
+            const int r = i / cn, j = i - r * cn;
+            a.out[(w0 + r) * (int64_t)a.L + c0 + j] = tile[r][j];
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace come
 
 using namespace come;
+
+int come::g_walk_staged = 1;  // come_set_option("walk_staged", 0): direct per-lane row stores
 
 extern "C" int come_random_walks(const int64_t *rowptr, const int32_t *col, int64_t V,
                                  const int32_t *starts, int64_t P, int L, float alpha,
@@ -103,10 +158,11 @@ extern "C" int come_random_walks(const int64_t *rowptr, const int32_t *col, int6
     if (rc) return rc;
     WalkArgs a{rowptr, col, starts, emit, out, V, P, walk_offset, seed, L,
                (uint32_t)ceil((double)alpha * 16777216.0)};
-    const int64_t blocks = (P + 255) / 256;
+    const int64_t blocks = (P + WALK_BLOCK - 1) / WALK_BLOCK;
     if (blocks > INT32_MAX) return set_error(COME_E_INVALID, "too many walks in one launch");
     void *kargs[] = {&a};
-    hipError_t e = hipLaunchKernel((void *)k_random_walks, dim3((unsigned)blocks), dim3(256),
-                                   kargs, 0, (hipStream_t)stream);
+    const void *k = g_walk_staged ? (const void *)k_random_walks_staged : (const void *)k_random_walks;
+    hipError_t e = hipLaunchKernel(k, dim3((unsigned)blocks), dim3(WALK_BLOCK), kargs, 0,
+                                   (hipStream_t)stream);
     return hip_error(e, "k_random_walks launch");
 }

@@ -110,3 +110,35 @@ def test_matches_reference_walker_distribution():
         return m / m.sum(1, keepdims=True)
     tv = 0.5 * np.abs(trans(ref) - trans(gw)).sum(1)
     assert tv.max() < 0.05, tv
+
+
+@pytest.mark.parametrize("P,L", [(1, 1), (255, 17), (257, 80), (10000, 33), (3000, 16)])
+def test_staged_output_matches_direct_stores(P, L):
+    """k_random_walks_staged (LDS-staged, coalesced row segments) vs k_random_walks (one store
+    per lane per step): the same Philox counters, so the walks must be identical -- including
+    invalid starts, dead ends (a node without neighbours), emit and ragged P / L."""
+    from come_amd import _lib
+    d = dev()
+    g = chung_lu(2000, 5.0, seed=P + L)
+    rowptr = np.concatenate([g.rowptr, [g.rowptr[-1]] * 3])  # 3 isolated nodes at the end
+    V = len(rowptr) - 1
+    rowptr_t = torch.from_numpy(rowptr).to(d)
+    col = torch.from_numpy(g.col.astype(np.int32)).to(d)
+    rng = np.random.RandomState(P)
+    s = rng.randint(0, V, P).astype(np.int32)
+    s[::7] = V - 1 - (np.arange(len(s[::7])) % 3)  # isolated: walk ends after one step
+    s[::11] = -1  # not a node: an empty walk
+    starts = torch.from_numpy(s).to(d)
+    emit = (torch.arange(V, device=d, dtype=torch.int32) * 5 + 2).contiguous()
+    try:
+        for kw in ({}, {"emit": emit}):
+            out = []
+            for opt in (0, 1):
+                _lib.set_option("walk_staged", opt)
+                out.append(gu.device_walks(rowptr_t, col, starts, L, alpha=0.15, seed=7,
+                                           walk_offset=5, **kw))
+            assert torch.equal(out[0], out[1]), (P, L, kw.keys())
+            w = out[1].cpu().numpy()
+            assert (w[::11] == -1).all()
+    finally:
+        _lib.set_option("walk_staged", 1)  # the default
