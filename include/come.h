@@ -209,7 +209,8 @@ int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int
  * defaults 16 / 12, 0 = no cap), "max_waves" (absolute cap on wavefronts in flight, 0 = none),
  * "o1_blocks_per_cu" (O1 grid cap in 4-wave workgroups per CU, 0 = 6), "resident_cap" (1 = also
  * clamp grids to the workgroups the occupancy API reports resident), "gmm_cov_async" (default 1: k_gmm_cov_async; 0 = k_gmm_cov_mfma), "community_async" (default 1:
- * k_community_async; 0 = the synchronous-staging k_community_mfma).
+ * k_community_async; 0 = the synchronous-staging k_community_mfma), "walk_staged" (default 1:
+ * LDS-staged walker output; 0 = one store per lane per step, identical walks).
  * Note: come_set_option() returns to the default only when set to the default value. */
 int come_set_option(const char *name, int value);
 
