@@ -91,8 +91,8 @@ __global__ void __launch_bounds__(256) k_random_walks(WalkArgs a) {
 // or past a dead end keep going through the chunk loop (they emit -1) so every lane reaches the
 // barriers.
 constexpr int WALK_BLOCK = 256;
-constexpr int WALK_CHUNK = 16;
 
+template <int WALK_CHUNK>
 __global__ void __launch_bounds__(WALK_BLOCK) k_random_walks_staged(WalkArgs a) {
     __shared__ int32_t tile[WALK_BLOCK][WALK_CHUNK + 1];  // +1: column writes hit distinct banks
     const int tid = threadIdx.x;
@@ -161,7 +161,11 @@ extern "C" int come_random_walks(const int64_t *rowptr, const int32_t *col, int6
     const int64_t blocks = (P + WALK_BLOCK - 1) / WALK_BLOCK;
     if (blocks > INT32_MAX) return set_error(COME_E_INVALID, "too many walks in one launch");
     void *kargs[] = {&a};
-    const void *k = g_walk_staged ? (const void *)k_random_walks_staged : (const void *)k_random_walks;
+    // walk_staged: 1 = 16-step slices (default), 2 = 8, 3 = 32 (A/B), 0 = direct stores
+    const void *k = g_walk_staged == 0   ? (const void *)k_random_walks
+                    : g_walk_staged == 2 ? (const void *)k_random_walks_staged<8>
+                    : g_walk_staged == 3 ? (const void *)k_random_walks_staged<32>
+                                         : (const void *)k_random_walks_staged<16>;
     hipError_t e = hipLaunchKernel(k, dim3((unsigned)blocks), dim3(WALK_BLOCK), kargs, 0,
                                    (hipStream_t)stream);
     return hip_error(e, "k_random_walks launch");

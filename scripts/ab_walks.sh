@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_walks.py -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_walks.log 2>&1 || { tail -30 gpurun_out/pytest_walks.log; exit 1; }
 tail -3 gpurun_out/pytest_walks.log
-for opt in 0 1 0 1; do
+for opt in ${OPTS:-0 1 0 1}; do
   timeout -k 10 300 python bench_aux.py --workload walks --steps 20 --warmup 3 --no-cpu-baseline \
     --opt walk_staged=$opt > gpurun_out/ab_walks_$opt.json 2> gpurun_out/ab_walks_$opt.err \
     || { tail -20 gpurun_out/ab_walks_$opt.err; exit 1; }
