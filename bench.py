@@ -6,18 +6,17 @@ One "step" = one O2 launch (come_sgns_o2, Hogwild, one wavefront per walk) over 
 steps -- the delta all-reduce of both embedding tables over RCCL.  Every rank trains its own walk
 shard (weak scaling).  Printed by rank 0: ONE JSON line (contract in the task statement), with
 `roofline` (dominant kernel: achieved algorithmic HBM bytes / launch time vs the 8 TB/s peak) and,
-at N = 1, `cpu_baseline` (the reference's own Cython train_o2, built by oracle/build_ref.py, timed
-on this host's cores with Python worker threads exactly as Context2Vec drives it).
+at N = 1, `cpu_baseline` (the builder's Hogwild C restatement of the reference's CPU path, timed on
+every core this process may use; its ratio to the reference's own Cython is calibrated in the
+container, profiles/r02_cpu_calibration.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
-import glob
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -47,70 +46,29 @@ def o2_pairs_of_lengths(lengths, w):
     return torch.where(l >= w + 1, full, small).sum()
 
 
-def cpu_reference_baseline(graph_walks_np, node_np, ctx_np, table_np, window, neg, lr,
-                           seconds, threads):
-    """Time the reference's Cython train_o2 (oracle/_ref) on host cores, driven like
-    Context2Vec.train (context_embeddings.py:72-98): worker threads, one call per walk, GIL
-    released inside.  Returns (pairs/s, pairs, walks) or None when the module is absent."""
-    import importlib.util
-    so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "training_sdg_inner*.so"))
-    if not so:
-        return None
-    spec = importlib.util.spec_from_file_location("training_sdg_inner", so[0])
-    ref = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(ref)
-
-    class Vocab(object):
-        __slots__ = ("index",)
-
-        def __init__(self, i):
-            self.index = i
-
-    cache = {}
-
-    def path_of(row):
-        out = []
-        for r in row:
-            if r < 0:
-                break
-            v = cache.get(r)
-            if v is None:
-                v = cache[r] = Vocab(int(r))
-            out.append(v)
-        return out
-
-    walks = [path_of(r) for r in graph_walks_np]
-    counter = {"next": 0, "pairs": 0, "walks": 0}
-    lock = threading.Lock()
-    deadline = [0.0]
-    d = node_np.shape[1]
-
-    def pairs_of(l):
-        return 2 * window * l - window * (window + 1) if l >= window + 1 else l * (l - 1)
-
-    def worker():
-        work = np.zeros(d, np.float32)
-        while True:
-            with lock:
-                i = counter["next"]
-                if i >= len(walks) or time.time() > deadline[0]:
-                    return
-                counter["next"] = i + 1
-            ref.train_o2(node_np, ctx_np, walks[i], lr, neg, window, table_np, py_alpha=1.0,
-                         py_size=d, py_work=work)
-            with lock:
-                counter["pairs"] += pairs_of(len(walks[i]))
-                counter["walks"] += 1
-
-    ts = [threading.Thread(target=worker, daemon=True) for _ in range(threads)]
+def cpu_port_baseline(walks_np, seeds_np, node_np, ctx_np, table_np, window, neg, lr, seconds,
+                      threads):
+    """Time the builder's Hogwild C restatement of the reference's CPU path
+    (oracle/come_oracle_mt.c: `threads` worker threads, one train_o2 walk per claim, plain racing
+    row updates -- context_embeddings.py:72-98 + pyx:454-509) on this host's cores.  The
+    reference itself never reaches the GPU box; the restatement's speed relative to the
+    reference's Cython train_o2 driven by Python threads is measured in the container by
+    scripts/calibrate_cpu.py (profiles/r02_cpu_calibration.json).  Returns (pairs/s, pairs,
+    walks, seconds, isa)."""
+    from oracle import oracle as orc
     t0 = time.time()
-    deadline[0] = t0 + seconds
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
+    pairs, done = orc.sgns_o2_hogwild(node_np, ctx_np, walks_np, seeds_np, window, neg, table_np,
+                                      lr, 1.0, threads, seconds)
     el = time.time() - t0
-    return counter["pairs"] / el, counter["pairs"], counter["walks"], el
+    return pairs / el, pairs, done, el, int(orc.lib().oracle_mt_isa())
+
+
+def calibration_ratio():
+    try:
+        c = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))
+        return float(c["ratio_restatement_over_cython"]), int(c["threads"])
+    except (OSError, ValueError, KeyError):
+        return None, None
 
 
 def main():
@@ -126,10 +84,11 @@ def main():
     ap.add_argument("--walk-length", type=int, default=80)
     ap.add_argument("--walks-per-step", type=int, default=1 << 17)
     ap.add_argument("--table-size", type=int, default=100_000_000)
-    ap.add_argument("--lr", type=float, default=0.025)
+    ap.add_argument("--lr", type=float, default=0.1)  # lr 0.1, alpha 1
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may use (affinity and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: blocking delta all-reduce instead of overlapping it with the next "
@@ -271,24 +230,26 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        sample = min(2 * B, walks_all.shape[0])  # ~2e8 pairs: the deadline ends the run
+        from oracle import oracle as orc
+        sample = min(2 * B, walks_all.shape[0])  # more than --cpu-seconds can finish
         wn = walks_all[:sample].cpu().numpy()
+        sn = seeds_all[:sample].cpu().numpy().view(np.uint64)
         node_h = np.ascontiguousarray(model.node_embedding.cpu().numpy())
         ctx_h = np.ascontiguousarray(model.context_embedding.cpu().numpy())
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        r = cpu_reference_baseline(wn, node_h, ctx_h, model.table_host, w, n, args.lr,
-                                   args.cpu_seconds, threads)
-        if r is not None:
-            rate, cp, cw, cel = r
-            cpu = {"value": rate, "unit": "pair-updates/s", "cores": threads,
-                   "kind": "reference",
-                   "sample": "reference Cython train_o2 (oracle/_ref, built from "
-                             "utils/training_sdg_inner.pyx) driven by %d Python threads like "
-                             "Context2Vec.train; %d walks / %d pair-updates of this workload "
-                             "(same graph, tables, negative table) in %.1fs" % (
-                                 threads, cw, cp, cel)}
-        else:
-            log("oracle/_ref absent: no reference CPU baseline")
+        threads = args.cpu_threads if args.cpu_threads > 0 else orc.usable_cpus()
+        rate, cp, cw, cel, isa = cpu_port_baseline(wn, sn, node_h, ctx_h, model.table_host, w, n,
+                                                   args.lr, args.cpu_seconds, threads)
+        ratio, rthreads = calibration_ratio()
+        cpu = {"value": rate, "unit": "pair-updates/s", "cores": threads, "kind": "port",
+               "nproc": orc.usable_cpus(), "visible_cpus": os.cpu_count(),
+               "sample": "builder's Hogwild C restatement of the reference CPU path "
+                         "(oracle/come_oracle_mt.c, %s build): %d threads, one train_o2 walk per "
+                         "claim as Context2Vec's workers; %d walks / %d pair-updates of this "
+                         "workload (same graph, walks, seeds, tables, negative table) in %.1fs. "
+                         "Calibration (profiles/r02_cpu_calibration.json, container, %s "
+                         "threads): restatement / reference Cython train_o2 = %s" % (
+                             "AVX2+FMA" if isa else "baseline-ISA", threads, cw, cp, cel,
+                             rthreads, "%.3f" % ratio if ratio else "n/a")}
 
     value = total_pairs / elapsed
     out = {
@@ -308,9 +269,11 @@ def main():
                 "tables initialised as the reference (node U(-1,1), ctx 0)",
         "config": {
             "workload": "%s: O2 SGNS over random walks, power-law %d nodes / %d "
-                        "edges, d=%d, negative=%d, window=%d, walk_length=%d, table_size=%d" % (
+                        "edges, d=%d, negative=%d, window=%d, walk_length=%d, table_size=%d, lr=%g, "
+                        "alpha=1" % (
                             "configs[4]/C5 (one GPU's shard)" if d == 256 and n == 10
-                            else "configs[2]/C3", V, g.num_edges, d, n, w, L, args.table_size),
+                            else "configs[2]/C3", V, g.num_edges, d, n, w, L, args.table_size,
+                            args.lr),
             "walks_per_step_per_gpu": B,
             "pairs_per_step_per_gpu": pairs_rank_step,
             "sync_every_steps": args.sync_every if world > 1 else None,

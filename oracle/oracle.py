@@ -40,8 +40,9 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(
-                os.path.join(HERE, "come_oracle.c")):
+        srcs = [os.path.join(HERE, s) for s in ("come_oracle.c", "come_oracle_mt.c")]
+        if not os.path.exists(LIB) or any(
+                os.path.exists(s) and os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs):
             build()
         L = ctypes.CDLL(LIB)
         P = ctypes.c_void_p
@@ -56,6 +57,12 @@ def lib():
         L.oracle_sgns_o1.restype = i64
         L.oracle_make_table.argtypes = [P, i64, P, u64, f64]
         L.oracle_min_margin.restype = f64
+        L.oracle_sgns_o2_hogwild.argtypes = [P, P, i64, i32, P, i64, i32, P, i32, i32, P, u64,
+                                             f32, f32, i32, f64, P]
+        L.oracle_sgns_o2_hogwild.restype = i64
+        L.oracle_sgns_o1_hogwild.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, f64,
+                                             P]
+        L.oracle_sgns_o1_hogwild.restype = i64
         _lib = L
     return _lib
 
@@ -105,6 +112,49 @@ def sgns_o1(node, edges, seeds, negative, table, lr, dot_mode=DOT_REF):
     seeds = np.ascontiguousarray(seeds, np.uint64)
     return int(lib().oracle_sgns_o1(_p(node), node.shape[1], _p(edges), edges.shape[0],
                                     _p(seeds), negative, _p(table), table.shape[0], lr, dot_mode))
+
+
+def sgns_o2_hogwild(node, ctx, walks, seeds, window, negative, table, lr, alpha, threads,
+                    max_seconds=0.0):
+    """Hogwild train_o2 on `threads` host threads, one walk per claim (come_oracle_mt.c,
+    context_embeddings.py:72-98).  Returns (pair updates, walks processed)."""
+    _chk(node, np.float32), _chk(ctx, np.float32), _chk(table, np.uint32)
+    walks = np.ascontiguousarray(walks, np.int32)
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    assert node.shape == ctx.shape and walks.shape[0] == seeds.shape[0]
+    done = np.zeros(1, np.int64)
+    pairs = lib().oracle_sgns_o2_hogwild(_p(node), _p(ctx), node.shape[0], node.shape[1],
+                                         _p(walks), walks.shape[0], walks.shape[1], _p(seeds),
+                                         window, negative, _p(table), table.shape[0], lr, alpha,
+                                         int(threads), float(max_seconds), _p(done))
+    return int(pairs), int(done[0])
+
+
+def sgns_o1_hogwild(node, edges, seeds, negative, table, lr, threads, max_seconds=0.0):
+    """Hogwild train_o1 on `threads` host threads, one edge per claim (node_embeddings.py:58-83).
+    Returns (pair updates, edges processed)."""
+    _chk(node, np.float32), _chk(table, np.uint32)
+    edges = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    done = np.zeros(1, np.int64)
+    pairs = lib().oracle_sgns_o1_hogwild(_p(node), node.shape[0], node.shape[1], _p(edges),
+                                         edges.shape[0], _p(seeds), negative, _p(table),
+                                         table.shape[0], lr, int(threads), float(max_seconds),
+                                         _p(done))
+    return int(pairs), int(done[0])
+
+
+def usable_cpus():
+    """CPUs this process may actually run on: the affinity mask, further limited by a cgroup v2
+    CPU quota (the GPU box shows 256 CPUs but grants a 16-CPU quota)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def make_table(counts_by_row, T, power=0.75):

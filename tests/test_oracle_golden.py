@@ -152,3 +152,65 @@ def test_karate_flow_oracle():
     x = orc.community_train(z["after_loop_node"], z["gmm_pi"], z["gmm_centroid"], z["gmm_inv"],
                             float(beta), float(lr), 5, chunksize=20)
     np.testing.assert_allclose(x, z["after_com_node"], atol=1e-6)
+
+
+# ---- the Hogwild CPU restatement (oracle/come_oracle_mt.c; bench.py's cpu_baseline) ----------
+
+@pytest.mark.parametrize("name", list(KAT_O2["names"]))
+def test_o2_hogwild_restatement_one_thread_matches_golden(name):
+    """One worker thread = walks in order (workers=1): the reference's own output, up to the
+    8-wide dot product's summation order (tier B)."""
+    z, pre = KAT_O2, "o2_%s_" % name
+    d, neg, w, V, L, P = [int(x) for x in z[pre + "params"]]
+    lr, alpha = [float(x) for x in z[pre + "lr_alpha"]]
+    node, ctx = z[pre + "node0"].copy(), z[pre + "ctx0"].copy()
+    pairs, done = orc.sgns_o2_hogwild(node, ctx, z[pre + "walks"], z[pre + "seeds"], w, neg,
+                                      z[pre + "table"], lr, alpha, threads=1)
+    assert done == P and pairs == orc.sgns_o2(node.copy(), ctx.copy(), z[pre + "walks"],
+                                              z[pre + "seeds"], w, neg, z[pre + "table"], lr,
+                                              alpha)
+    np.testing.assert_allclose(node, z[pre + "node1"], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(ctx, z[pre + "ctx1"], rtol=0, atol=1e-3)
+
+
+@pytest.mark.parametrize("name", list(KAT_O1["names"]))
+def test_o1_hogwild_restatement_one_thread_matches_golden(name):
+    z, pre = KAT_O1, "o1_%s_" % name
+    d, neg, V, E = [int(x) for x in z[pre + "params"]]
+    node = z[pre + "node0"].copy()
+    pairs, done = orc.sgns_o1_hogwild(node, z[pre + "edges"], z[pre + "seeds"], neg,
+                                      z[pre + "table"], float(z[pre + "lr"][0]), threads=1)
+    assert pairs == 2 * E and done == E
+    np.testing.assert_allclose(node, z[pre + "node1"], rtol=0, atol=1e-3)
+
+
+def test_o2_hogwild_restatement_threads_disjoint_rows_exact():
+    """Walks that share no row cannot race when they draw no negatives (n = 0), so 8 threads give
+    exactly the 1-thread result."""
+    rng = np.random.RandomState(3)
+    V, d, P, L = 4000, 64, 64, 20
+    walks = np.arange(P * L, dtype=np.int32).reshape(P, L)  # every row distinct
+    table = np.arange(P * L, V, dtype=np.uint32)            # negatives outside the walks
+    seeds = rng.randint(0, 2 ** 48, P).astype(np.uint64)
+    node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+    outs = []
+    for thr in (1, 8):
+        node, ctx = node0.copy(), np.zeros_like(node0)
+        pairs, done = orc.sgns_o2_hogwild(node, ctx, walks, seeds, 3, 0, table, 0.1, 1.0, thr)
+        assert done == P
+        outs.append((node, ctx))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_o2_hogwild_restatement_deadline_and_threads():
+    """max_seconds stops the claiming early; every walk is processed once otherwise."""
+    rng = np.random.RandomState(4)
+    V, d, P, L = 2000, 32, 400, 30
+    walks = rng.randint(0, V, (P, L)).astype(np.int32)
+    seeds = rng.randint(0, 2 ** 48, P).astype(np.uint64)
+    table = orc.make_table(rng.randint(1, 20, V), 10000)
+    node, ctx = rng.uniform(-1, 1, (V, d)).astype(np.float32), np.zeros((V, d), np.float32)
+    pairs, done = orc.sgns_o2_hogwild(node, ctx, walks, seeds, 5, 5, table, 0.05, 1.0, 4)
+    assert done == P and pairs == P * (2 * 5 * L - 5 * 6)
+    assert np.isfinite(node).all() and np.isfinite(ctx).all()
+    assert orc.usable_cpus() >= 1
