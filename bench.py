@@ -95,6 +95,11 @@ def main():
                          "batch")
     ap.add_argument("--packed-table", action="store_true",
                     help="draw negatives from the exact packed table (come_pack_table)")
+    ap.add_argument("--hot-p", type=float, default=None,
+                    help="rows holding >= this share of the negative table are updated with "
+                         "float atomics (default training_sdg_inner.DEFAULT_HOT_P; 0 = none)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="per-call launch option k=v (come_launch_opts field), for A/B runs")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
@@ -150,10 +155,19 @@ def main():
     neg_table = model.table_packed if args.packed_table and model.table_packed is not None \
         else model.table
 
-    def step(s):
+    # target-row updates applied by the timed launches (the +-6 skip, pyx:141, leaves a target
+    # row unwritten, so the bytes a launch must move depend on the data): counted in-kernel
+    upd_count = torch.zeros(1, dtype=torch.int64, device=dev)
+    opts = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)} or None
+    hot_p = tsi.DEFAULT_HOT_P if args.hot_p is None else args.hot_p
+    hot = model.hot_rows(hot_p)
+    n_hot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
+
+    def step(s, count=False):
         tsi.sgns_o2(model.node_embedding, model.context_embedding, walks_all[s * B:(s + 1) * B],
                     seeds_all[s * B:(s + 1) * B], w, n, neg_table, args.lr, 1.0,
-                    tsi.MODE_HOGWILD)
+                    tsi.MODE_HOGWILD, opts=opts, update_count=upd_count if count else None,
+                    hot=hot)
 
     stream = torch.cuda.current_stream(dev)
     def exchange():
@@ -181,7 +195,7 @@ def main():
     for k in range(args.steps):
         s = args.warmup + k
         ev[k][0].record(stream)
-        step(s)
+        step(s, count=True)
         ev[k][1].record(stream)
         if sync is not None and (k + 1) % args.sync_every == 0:
             exchange()
@@ -212,16 +226,23 @@ def main():
             dist.destroy_process_group()
         return
 
-    bytes_per_pair = 2 * (2 + n) * d * 4  # in row r+w, (1+n) out rows r+w
+    # SURVEY.md §8d algorithmic bytes per pair: the input row read + written and the (1+n) output
+    # rows read + written = 2 (2+n) d 4 (7,168 B at d=128, n=5) when no target is skipped.  A
+    # target whose |dot| >= 6 is skipped (pyx:141) and its row is read but not written, so per
+    # launch: pairs * (3+n) d 4 (reads + the unconditional input write, pyx:149) + updates * d 4.
+    bytes_per_pair_max = 2 * (2 + n) * d * 4
     pairs_rank_step = float(np.mean(pairs_per_step[args.warmup:]))
+    updates_rank_step = float(upd_count.item()) / args.steps
+    alg_bytes_step = pairs_rank_step * (3 + n) * d * 4 + updates_rank_step * d * 4
+    bytes_per_pair = alg_bytes_step / pairs_rank_step
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
-    achieved = bytes_per_pair * pairs_rank_step / avg_kernel_s / 1e9
+    achieved = alg_bytes_step / avg_kernel_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if (tj.get("walks_per_launch") == B and tj.get("dim") == d
-                    and tj.get("negative") == n
+                    and tj.get("negative") == n and tj.get("lr") == args.lr
                     and kernel_name(d, n).replace(" ", "") in
                     tj.get("kernel", "").replace(" ", "")):
                 traffic = tj.get("hbm_bytes_per_launch")
@@ -275,6 +296,8 @@ def main():
                             else "configs[2]/C3", V, g.num_edges, d, n, w, L, args.table_size,
                             args.lr),
             "walks_per_step_per_gpu": B,
+            "launch_opts": opts,
+            "hot_rows": {"share_threshold": hot_p, "rows": n_hot},
             "pairs_per_step_per_gpu": pairs_rank_step,
             "sync_every_steps": args.sync_every if world > 1 else None,
             "parallelism": "walk-shard dp%d + %s delta all-reduce (%s)" % (
@@ -291,6 +314,8 @@ def main():
             "traffic": traffic,
             "kernel": kernel_name(d, n),
             "bytes_per_pair": bytes_per_pair,
+            "bytes_per_pair_no_skip": bytes_per_pair_max,
+            "target_updates_per_pair": updates_rank_step / pairs_rank_step,
             "avg_kernel_ms": avg_kernel_s * 1e3,
         },
         "cpu_baseline": cpu,

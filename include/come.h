@@ -12,7 +12,11 @@
  *    reference's numpy arrays have (pyx:410-411,457-459).
  *  - `stream` is a hipStream_t passed as void* (NULL = the default stream).  Calls are
  *    asynchronous on that stream, capture-safe (no allocation / synchronisation inside) once
- *    come_init() has run for the device, and reentrant per stream.
+ *    come_init() has run for the device, and reentrant per stream.  Launch options: each call
+ *    reads ONE consistent snapshot of the process-wide options (come_set_option, mutex-guarded:
+ *    a change applies to calls that start after it returns, never half of one); the *_ex entry
+ *    points take per-call options instead (come_launch_opts), so concurrent callers with
+ *    different options do not interfere.
  *  - Return value: 0 = ok, < 0 = error (COME_E_*); come_last_error() returns a message
  *    (thread-local).  The reference checks nothing (bounds checks off, cython_utils.py:7); this
  *    library validates shapes/arguments on the host and never reads or writes out of bounds on
@@ -198,21 +202,78 @@ int come_delta_begin(const float *W, const float *S, float *D, float *Down, int6
 int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int64_t n,
                    void *stream);
 
-/* ---- Tuning ----
- * Process-wide launch knobs for experiments (0 = automatic): "o2_kernel" (1 direct, 2 ring),
- * "o2_blocks_per_cu", "o2_waves_per_block", "o2_plain_writeback" (1 = Hogwild with plain-store
- * write-back of cached rows: faster but loses concurrent updates; not the default), "o2_static"
- * (1 = static grid-stride walk assignment instead of the default device work queue),
- * "o2_pair_atomics" (1 = Hogwild node rows get one float-atomic add per pair instead of one
- * delta per window residency), "rows_per_wave" / "o1_rows_per_wave" (Hogwild launches keep at
- * most V / rows_per_wave wavefronts in flight so updates stay sparse on small vocabularies;
- * defaults 16 / 12, 0 = no cap), "max_waves" (absolute cap on wavefronts in flight, 0 = none),
- * "o1_blocks_per_cu" (O1 grid cap in 4-wave workgroups per CU, 0 = 6), "resident_cap" (1 = also
- * clamp grids to the workgroups the occupancy API reports resident), "gmm_cov_async" (default 1: k_gmm_cov_async; 0 = k_gmm_cov_mfma), "community_async" (default 1:
- * k_community_async; 0 = the synchronous-staging k_community_mfma), "walk_staged" (default 1:
- * LDS-staged walker output; 0 = one store per lane per step, identical walks).
- * Note: come_set_option() returns to the default only when set to the default value. */
+/* ---- Launch options ----
+ * Kernel-selection and grid knobs (0 = automatic unless stated):
+ *   o2_kernel           1 = direct kernel, 2 = LDS-ring kernel (automatic: ring when it fits)
+ *   o2_blocks_per_cu    O2 grid cap in workgroups per CU
+ *   o2_waves_per_block  1 or 2 (automatic 2)
+ *   o2_static           1 = static grid-stride walk assignment instead of the device work queue
+ *   rows_per_wave / o1_rows_per_wave  Hogwild launches keep at most V / rows_per_wave
+ *                       wavefronts in flight so updates stay sparse on small vocabularies
+ *                       (defaults 16 / 12; 0 = no cap)
+ *   max_waves           absolute cap on wavefronts in flight (0 = none)
+ *   o1_blocks_per_cu    O1 grid cap in 4-wave workgroups per CU (0 = 6)
+ *   resident_cap        1 = also clamp grids to the workgroups the occupancy API reports resident
+ *   community_async     default 1: k_community_async; 0 = synchronous-staging k_community_mfma
+ *   gmm_cov_async       default 1: k_gmm_cov_async; 0 = k_gmm_cov_mfma
+ *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
+ *                       0 = one store per lane per step (identical walks)
+ *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
+ *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
+ *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
+ *                       row updates the launch applied (positive + negatives that passed the
+ *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM
+ *                       traffic is counted from.  NULL = not counted. */
+typedef struct come_launch_opts {
+    int o2_kernel;
+    int o2_blocks_per_cu;
+    int o2_waves_per_block;
+    int o2_static;
+    int rows_per_wave;
+    int o1_rows_per_wave;
+    int max_waves;
+    int o1_blocks_per_cu;
+    int resident_cap;
+    int community_async;
+    int gmm_cov_async;
+    int walk_staged;
+    int o2_fresh_loads;
+    int o2_atomic_writeback;
+    uint64_t *o2_update_count;
+} come_launch_opts;
+
+/* Fills *out with the current process-wide options (o2_update_count = NULL). */
+int come_get_options(come_launch_opts *out);
+
+/* Sets one process-wide option by field name (thread-safe; calls already inside the library
+ * keep the snapshot they took). */
 int come_set_option(const char *name, int value);
+
+/* come_sgns_o2 with the contended-row bitmap and per-call options.
+ * hot_rows  device uint32 [ceil(V / 32)] (come_hot_rows), or NULL: in COME_MODE_HOGWILD the rows
+ *           whose bit is set are read right before each pair and updated with float-atomic
+ *           deltas at the memory side (no concurrent update lost, no stale cached copy); the
+ *           other rows are cached per wavefront and written back with plain stores.  Ignored in
+ *           COME_MODE_SEQUENTIAL.  With NULL every row is treated as cold, which on graphs with
+ *           hubs trains measurably worse than the reference's Hogwild (tests/test_gpu_tierc.py).
+ * opts      per-call launch options, or NULL = the process-wide ones. */
+int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,
+                    int L, const uint64_t *seeds, int window, int negative,
+                    const uint32_t *table, uint64_t T, float lr, float alpha, int mode,
+                    const uint32_t *hot_rows, const come_launch_opts *opts, void *stream);
+
+/* Contended rows of a negative-sampling table: counts[v] = number of slots of table[0, T) holding
+ * v (device uint32 [V] scratch, overwritten) and hot_bits (device uint32 [ceil(V / 32)]) bit v set
+ * iff counts[v] >= min_count.  A row's share of the table is its draw probability as a negative
+ * and grows with its count (degree), i.e. with how often walks visit it.  Asynchronous. */
+int come_hot_rows(const uint32_t *table, uint64_t T, int64_t V, uint64_t min_count,
+                  uint32_t *counts, uint32_t *hot_bits, void *stream);
+/* come_sgns_o1 with the contended-row bitmap (Hogwild: an update of a hot endpoint row is a
+ * float-atomic delta) and per-call options (opts may be NULL = process-wide). */
+int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
+                    const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
+                    float lr, int mode, const uint32_t *hot_rows, const come_launch_opts *opts,
+                    void *stream);
 
 /* ---- Host helpers ---- */
 

@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcome.so")
+# COME_LIB_PATH: an alternative in-tree build of the same library (A/B experiments only)
+LIB_PATH = os.environ.get("COME_LIB_PATH") or os.path.join(HERE, "libcome.so")
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
@@ -21,7 +22,19 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_pyrandom_draw", "come_graph_from_edges", "come_read_int_rows",
            "come_write_int_rows", "come_save_embedding", "come_format_f32",
            "come_gmm_estep", "come_gmm_scatter", "come_pack_table",
-           "come_delta_begin", "come_delta_end")
+           "come_delta_begin", "come_delta_end", "come_get_options", "come_sgns_o2_ex",
+           "come_sgns_o1_ex", "come_hot_rows")
+
+OPTION_FIELDS = ("o2_kernel", "o2_blocks_per_cu", "o2_waves_per_block",
+                 "o2_static", "rows_per_wave", "o1_rows_per_wave",
+                 "max_waves", "o1_blocks_per_cu", "resident_cap", "community_async",
+                 "gmm_cov_async", "walk_staged", "o2_fresh_loads", "o2_atomic_writeback")
+
+
+class LaunchOpts(ctypes.Structure):
+    """come_launch_opts (include/come.h): per-call launch options of the *_ex entry points."""
+    _fields_ = [(f, ctypes.c_int) for f in OPTION_FIELDS] + [("o2_update_count",
+                                                             ctypes.c_void_p)]
 
 _lib = None
 
@@ -68,6 +81,11 @@ def lib():
     L.come_count_o2_pairs.argtypes = [P, i64, i32, i32]
     L.come_count_o2_pairs.restype = i64
     L.come_set_option.argtypes = [ctypes.c_char_p, i32]
+    L.come_get_options.argtypes = [P]
+    L.come_sgns_o2_ex.argtypes = [P, P, i64, i32, P, i64, i32, P, i32, i32, P, u64, f32, f32, i32,
+                                  P, P, P]
+    L.come_hot_rows.argtypes = [P, u64, i64, u64, P, P, P]
+    L.come_sgns_o1_ex.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, P, P, P]
     cp = ctypes.c_char_p
     L.come_random_walks.argtypes = [P, P, i64, P, i64, i32, f32, u64, i64, P, P, P]
     L.come_walks_reference.argtypes = [P, P, i64, i32, P, P, i32, f64, P, i32, P]
@@ -103,5 +121,19 @@ def stream_handle(device=None):
 
 
 def set_option(name, value):
-    """Launch tuning knob (see include/come.h come_set_option)."""
+    """Process-wide launch option (see include/come.h come_set_option)."""
     check(lib().come_set_option(name.encode(), int(value)), "come_set_option(%s)" % name)
+
+
+def launch_opts(update_count=None, **overrides):
+    """A LaunchOpts holding the current process-wide options with `overrides` applied, and
+    o2_update_count = the address of `update_count` (a CUDA int64 tensor of one element)."""
+    o = LaunchOpts()
+    check(lib().come_get_options(ctypes.byref(o)), "come_get_options")
+    for k, v in overrides.items():
+        if k not in OPTION_FIELDS:
+            raise ValueError("unknown launch option %r" % k)
+        setattr(o, k, int(v))
+    if update_count is not None:
+        o.o2_update_count = update_count.data_ptr()
+    return o

@@ -58,13 +58,14 @@ class Context2Vec(object):
             pairs = tsi.count_o2_pairs(rows, self.window_size)
             n_valid = int((rows >= 0).sum())
         mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
+        hot = None if self.deterministic else model.hot_rows()
         for s in range(0, rows.shape[0], self.batch_walks):
             w = rows[s:s + self.batch_walks]
             w = w.contiguous() if isinstance(w, torch.Tensor) else \
                 torch.from_numpy(np.ascontiguousarray(w)).to(dev)
             sd = torch.from_numpy(seeds[s:s + self.batch_walks].view(np.int64)).to(dev)
             tsi.sgns_o2(model.node_embedding, model.context_embedding, w, sd, self.window_size,
-                        self.negative, model.negative_table(), self.lr, alpha, mode)
+                        self.negative, model.negative_table(), self.lr, alpha, mode, hot=hot)
         torch.cuda.synchronize(dev)
         elapsed = time.time() - start
         nodes = n_valid + node_count

@@ -858,11 +858,6 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float
 
 }  // namespace come
 
-namespace come {
-int g_comm_async = 1;  // come_set_option("community_async", 0): synchronous k_community_mfma
-int g_cov_async = 1;   // come_set_option("gmm_cov_async", 0): synchronous k_gmm_cov_mfma
-}
-
 using namespace come;
 
 extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, const float *mu,
@@ -877,7 +872,7 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     if (rc) return rc;
     CommArgs a{x, pi, mu, inv_cov, V, d, K, (float)((double)beta / (double)K), lr, iters};
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 &&
-        ((uintptr_t)mu % 16) == 0 && g_comm_async) {
+        ((uintptr_t)mu % 16) == 0 && current_opts().community_async) {
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(d == 64 ? CommAsync<64>::LDS_FLOATS
                                                             : CommAsync<128>::LDS_FLOATS);
@@ -993,14 +988,15 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const int used = V == 0 ? 1 : (int)((V + per - 1) / per);
     CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K};
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
+    const bool cov_async = current_opts().gmm_cov_async != 0;
     void (*kern)(CovArgs) =
         !mfma ? k_gmm_cov_valu
-              : g_cov_async ? (d == 64 ? k_gmm_cov_async<64, kCovKPB>
+              : cov_async ? (d == 64 ? k_gmm_cov_async<64, kCovKPB>
                                        : k_gmm_cov_async<128, kCovKPB>)
                             : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
     const int threads = !mfma ? 256 : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
     size_t lds = 0;
-    if (mfma && g_cov_async) {
+    if (mfma && cov_async) {
         lds = sizeof(float) * (size_t)(2 * kCovAsyncRB * d + 2 * 64);
         static bool attr = false;
         if (!attr) {
@@ -1011,7 +1007,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
             attr = true;
         }
     }
-    const unsigned gx = (mfma && g_cov_async) ? (unsigned)((K + kCovKPB - 1) / kCovKPB) : K;
+    const unsigned gx = (mfma && cov_async) ? (unsigned)((K + kCovKPB - 1) / kCovKPB) : K;
     hipLaunchKernelGGL(kern, dim3(gx, used), dim3(threads), lds, (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;

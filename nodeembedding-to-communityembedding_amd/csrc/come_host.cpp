@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdarg.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -77,9 +78,6 @@ struct Scratch {
 static std::unordered_map<void *, Scratch> g_scratch[kMaxDevices][kScratchSlots];
 static std::mutex g_scratch_mu;
 
-float *o2_scratch(int device, void *stream, size_t bytes) {
-    return stream_scratch(device, stream, kScratchO2Snapshots, bytes);
-}
 
 float *stream_scratch(int device, void *stream, int slot, size_t bytes) {
     if (slot < 0 || slot >= kScratchSlots) return nullptr;
@@ -103,9 +101,65 @@ int64_t *launch_counter(int device, void *stream) {
     return c;
 }
 
+// ---- process-wide launch options (come_set_option / come_get_options) ----
+static std::mutex g_opts_mu;
+static come_launch_opts g_opts = [] {
+    come_launch_opts o;
+    memset(&o, 0, sizeof(o));
+    // Hogwild concurrency: at most max(1, V / rows_per_wave) wavefronts in flight.  Hogwild
+    // needs sparse updates: with every wavefront holding ~17 rows (O2: the 2w+1 window, the
+    // positive, the pair's negatives; O1 12), a vocabulary smaller than ~16 rows per wavefront
+    // in flight has most rows held by several wavefronts at once and the embeddings stop
+    // converging -- measured on a 2,000-node planted partition (scripts/diag_hogwild.py):
+    // community NMI 0.75 with 6,000 waves in flight, 0.97-0.98 with <= V/16 (= the sequential
+    // run's 0.97); at 100,000 nodes the cap is inactive (V/16 > occupancy) and NMI 0.99 either way.
+    o.rows_per_wave = 16;
+    o.o1_rows_per_wave = 12;
+    o.community_async = 1;
+    o.gmm_cov_async = 1;
+    o.walk_staged = 1;
+    return o;
+}();
+
+come_launch_opts current_opts() {
+    std::lock_guard<std::mutex> lock(g_opts_mu);
+    come_launch_opts o = g_opts;
+    o.o2_update_count = nullptr;
+    return o;
+}
+
 }  // namespace come
 
 using namespace come;
+
+extern "C" int come_get_options(come_launch_opts *out) {
+    if (!out) return set_error(COME_E_INVALID, "null options pointer");
+    *out = current_opts();
+    return COME_OK;
+}
+
+extern "C" int come_set_option(const char *name, int value) {
+    if (!name) return set_error(COME_E_INVALID, "null option name");
+#define COME_OPT(f) {#f, offsetof(come_launch_opts, f)}
+    static const struct {
+        const char *k;
+        size_t off;
+    } fields[] = {COME_OPT(o2_kernel),        COME_OPT(o2_blocks_per_cu),
+                  COME_OPT(o2_waves_per_block), COME_OPT(o2_static),
+                  COME_OPT(rows_per_wave),    COME_OPT(o1_rows_per_wave),
+                  COME_OPT(max_waves),        COME_OPT(o1_blocks_per_cu),
+                  COME_OPT(resident_cap),     COME_OPT(community_async),
+                  COME_OPT(gmm_cov_async),    COME_OPT(walk_staged),
+                  COME_OPT(o2_fresh_loads),   COME_OPT(o2_atomic_writeback)};
+#undef COME_OPT
+    for (const auto &f : fields)
+        if (!strcmp(f.k, name)) {
+            std::lock_guard<std::mutex> lock(g_opts_mu);
+            *reinterpret_cast<int *>(reinterpret_cast<char *>(&g_opts) + f.off) = value;
+            return COME_OK;
+        }
+    return set_error(COME_E_INVALID, "unknown option '%s'", name);
+}
 
 extern "C" int come_abi_version(void) { return COME_ABI_VERSION; }
 

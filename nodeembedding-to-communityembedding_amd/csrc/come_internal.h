@@ -25,14 +25,13 @@ int num_cus(int device);                        // multiprocessor count (cached)
 // statically).  Enqueues a hipMemsetAsync: capture-safe.
 int64_t *launch_counter(int device, void *stream);
 // Device scratch of at least `bytes` for launches on `stream` (library-owned, one buffer per
-// device and stream, grows on demand: the first call at a larger size allocates, so capture a
-// stream only after a warm-up call of the same shape).
-float *o2_scratch(int device, void *stream, size_t bytes);
-constexpr int kScratchO2Snapshots = 0, kScratchGmmFlags = 1, kScratchSlots = 2;
+// device, stream and slot, grows on demand: the first call at a larger size allocates, so capture
+// a stream only after a warm-up call of the same shape).
+constexpr int kScratchGmmFlags = 0, kScratchSlots = 1;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
-extern int g_walk_staged;  // walker output staging (come_set_option "walk_staged")
-extern int g_comm_async;  // community gradient kernel choice (come_set_option "community_async")
-extern int g_cov_async;   // GMM scatter kernel choice (come_set_option "gmm_cov_async")
+// One consistent snapshot of the process-wide launch options (come_set_option; mutex-guarded).
+// Every entry point takes it once at its start, or uses the caller's come_launch_opts (*_ex).
+come_launch_opts current_opts();
 
 // Lemire fastmod: a % d for 32-bit a, d >= 1, from one 64-bit multiply-high.  m = 0 encodes
 // "d >= 2^32" (then a % d == a for every 32-bit a).

@@ -9,35 +9,15 @@
 
 namespace come {
 
-constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr size_t kRingMaxWaveBytes = 40 * 1024;
 
-// Tuning / experiment knobs (come_set_option); 0 = automatic.
-static int g_opt_o2_kernel = 0;         // 1 = direct kernel, 2 = ring kernel
-static int g_opt_o2_blocks_per_cu = 0;  // grid cap override
-static int g_opt_o2_plain_writeback = 0;  // 1 = Hogwild with plain-store write-back (lossy)
-static int g_opt_o2_waves_per_block = 0;
-static int g_opt_o2_static = 0;  // 1 = grid-stride walk assignment instead of the work queue
-static int g_opt_o2_pair_atomics = 0;  // 1 = HOG node rows: one atomic per pair (no snapshots)
-// Hogwild concurrency: at most max(1, V / rows_per_wave) wavefronts in flight (0 = no V-based
-// cap) and at most max_waves (0 = the hardware's occupancy).  Hogwild needs sparse updates: with
-// every wavefront holding ~17 rows (O2: the 2w+1 window, the positive, the pair's negatives; O1
-// 12), a vocabulary smaller than ~16 rows per wavefront in flight has most rows held by several
-// wavefronts at once and the embeddings stop converging -- measured on a 2,000-node planted
-// partition (scripts/diag_hogwild.py): community NMI 0.75 with 6,000 waves in flight, 0.97-0.98
-// with <= V/16 (= the sequential run's 0.97); at 100,000 nodes the cap is inactive (V/16 >
-// occupancy) and NMI 0.99 either way.
-static int g_opt_rows_per_wave = 16;     // O2
-static int g_opt_o1_rows_per_wave = 12;  // O1
-static int g_opt_max_waves = 0;
-static int g_opt_o1_blocks_per_cu = 0;    // O1 grid cap (0 = 6 four-wave workgroups per CU)
-static int g_opt_resident_cap = 0;        // 1 = clamp grids to resident workgroups (A/B)
-
 // Cap on the number of workgroups of a Hogwild launch (0 = none).
-static int64_t hog_max_blocks(int64_t V, int wpb, int rows_per_wave) {
+// Launch knobs come from the caller's come_launch_opts or one snapshot of the process-wide ones
+// (come_set_option); see include/come.h for their meaning.
+static int64_t hog_max_blocks(const come_launch_opts &o, int64_t V, int wpb, int rows_per_wave) {
     int64_t waves = 0;
     if (rows_per_wave > 0) waves = V / rows_per_wave > 1 ? V / rows_per_wave : 1;
-    if (g_opt_max_waves > 0 && (waves == 0 || g_opt_max_waves < waves)) waves = g_opt_max_waves;
+    if (o.max_waves > 0 && (waves == 0 || o.max_waves < waves)) waves = o.max_waves;
     return waves > 0 ? (waves + wpb - 1) / wpb : 0;
 }
 
@@ -79,8 +59,9 @@ static int resident_blocks(void *fn, int threads, size_t lds) {
 // Launch `fn` with one wavefront per unit (walk / edge), `wpb` wavefronts per workgroup, grid
 // capped at `blocks_per_cu` workgroups per CU and at what is resident (grid-stride beyond);
 // SEQUENTIAL = one wavefront.
-static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int blocks_per_cu,
-                  size_t lds_bytes, void *stream, int64_t max_blocks = 0) {
+static int launch(const come_launch_opts &o, void *fn, void *args, int64_t units, int mode,
+                  int wpb, int blocks_per_cu, size_t lds_bytes, void *stream,
+                  int64_t max_blocks = 0) {
     int dev = 0;
     int rc = ensure_init(&dev);
     if (rc) return rc;
@@ -91,7 +72,7 @@ static int launch(void *fn, void *args, int64_t units, int mode, int wpb, int bl
     } else {
         int64_t blocks = (units + wpb - 1) / wpb;
         const int res = resident_blocks(fn, 64 * wpb, lds_bytes);
-        if (res > 0 && blocks_per_cu > res && g_opt_resident_cap) blocks_per_cu = res;
+        if (res > 0 && blocks_per_cu > res && o.resident_cap) blocks_per_cu = res;
         int64_t cap = (int64_t)num_cus(dev) * blocks_per_cu;
         if (max_blocks > 0 && max_blocks < cap) cap = max_blocks;
         if (blocks > cap) blocks = cap;
@@ -135,10 +116,12 @@ static bool aligned_for(const void *p, int d) {
     return ((uintptr_t)p % bytes) == 0;
 }
 
-extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks,
-                            int64_t P, int L, const uint64_t *seeds, int window, int negative,
-                            const uint32_t *table, uint64_t T, float lr, float alpha, int mode,
-                            void *stream) {
+extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const int32_t *walks,
+                               int64_t P, int L, const uint64_t *seeds, int window, int negative,
+                               const uint32_t *table, uint64_t T, float lr, float alpha, int mode,
+                               const uint32_t *hot_rows, const come_launch_opts *opts,
+                               void *stream) {
+    const come_launch_opts o = opts ? *opts : current_opts();
     int packed = 0;
     int rc = check_common(V, d, negative, table, T, mode, packed);
     if (rc) return rc;
@@ -150,52 +133,49 @@ extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int
     if (!aligned_for(node, d) || !aligned_for(ctx, d))
         return set_error(COME_E_INVALID, "node/ctx must be 16-byte aligned for d=%d", d);
     O2Args a{node, ctx, walks, seeds, table, V, P, L, d, window, negative, lr, alpha,
-             make_fastmod(T), packed, nullptr, nullptr};
+             make_fastmod(T), packed, nullptr,
+             reinterpret_cast<unsigned long long *>(o.o2_update_count), o.o2_fresh_loads,
+             o.o2_atomic_writeback, mode == COME_MODE_HOGWILD ? hot_rows : nullptr};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
     const int mi = maxn_index(negative);
     const bool hog = mode == COME_MODE_HOGWILD;
-    // LDS ring of the cached kernel: (2w+1) rows + their ids, per wave
+    if (hog && o.o2_kernel != 1 && window <= 31) {
+        // streaming Hogwild kernel: 4-wave workgroups, 8 per CU (= its 8 waves per SIMD at
+        // d <= 128, n <= 5; measured 6 / 7 / 8 -> 122 / 115 / 108 ms per C3 launch), device work
+        // queue
+        int dev = 0;
+        rc = ensure_init(&dev);
+        if (rc) return rc;
+        if (!o.o2_static) a.counter = launch_counter(dev, stream);  // else grid-stride
+        return launch(o, ks.o2_stream[full][mi], &a, P, mode, 4,
+                      o.o2_blocks_per_cu > 0 ? o.o2_blocks_per_cu : 8, 0, stream,
+                      hog_max_blocks(o, V, 4, o.rows_per_wave));
+    }
+    // LDS ring of the sequential kernel: (2w+1) rows + their ids
     const int rs = 2 * window + 1;
     const size_t wave_bytes = 4 * (size_t)((rs * d + 3) & ~3);
     const bool ring_ok = rs <= 64 && wave_bytes <= kRingMaxWaveBytes;
-    if (g_opt_o2_kernel != 1 && ring_ok) {
-        // __launch_bounds__(128): at most 2 wavefronts per workgroup
-        const int wpb = g_opt_o2_waves_per_block == 1 ? 1 : 2;
-        const size_t lds = wave_bytes * (hog ? wpb : 1);
-        // 24 wavefronts per CU measured best on MI355X (d=128, n=5: 16/20/24/28 waves ->
-        // 141/123/110/132 ms per 1e8-pair launch with the first write-back; with the work queue
-        // and delta write-back 20/22/24/26 -> 111.0/104.6/100.3/100.3 ms, scripts/ab_o2.py).
-        int per_cu = (int)(kLdsPerCu / (wave_bytes * wpb));
-        per_cu = per_cu < 1 ? 1 : (per_cu > 24 / wpb ? 24 / wpb : per_cu);
-        if (g_opt_o2_blocks_per_cu > 0) per_cu = g_opt_o2_blocks_per_cu;
-        const int variant = (hog && !g_opt_o2_plain_writeback) ? 1 : 0;
-        if (hog) {
-            int dev = 0;
-            rc = ensure_init(&dev);
-            if (rc) return rc;
-            if (!g_opt_o2_static) a.counter = launch_counter(dev, stream);  // else grid-stride
-            if (variant == 1 && !g_opt_o2_pair_atomics) {
-                // entry snapshots, one [2w+1][d] region per wavefront of the (capped) grid
-                int64_t blocks = (P + wpb - 1) / wpb;
-                int64_t cap = (int64_t)num_cus(dev) * per_cu;
-                const int64_t hcap = hog_max_blocks(V, wpb, g_opt_rows_per_wave);
-                if (hcap > 0 && hcap < cap) cap = hcap;
-                if (blocks > cap) blocks = cap;
-                a.orig = o2_scratch(dev, stream, (size_t)blocks * wpb * rs * d * sizeof(float));
-            }
-        }
-        return launch(ks.o2_ring[full][mi][variant], &a, P, mode, wpb, per_cu, lds, stream,
-                      hog ? hog_max_blocks(V, wpb, g_opt_rows_per_wave) : 0);
-    }
-    return launch(ks.o2_direct[full][mi], &a, P, mode, 4,
-                  g_opt_o2_blocks_per_cu > 0 ? g_opt_o2_blocks_per_cu : 6, 0, stream,
-                  hog ? hog_max_blocks(V, 4, g_opt_rows_per_wave) : 0);
+    if (!hog && o.o2_kernel != 1 && ring_ok)
+        return launch(o, ks.o2_ring[full][mi], &a, P, mode, 1, 1, wave_bytes, stream);
+    return launch(o, ks.o2_direct[full][mi], &a, P, mode, 4,
+                  o.o2_blocks_per_cu > 0 ? o.o2_blocks_per_cu : 6, 0, stream,
+                  hog ? hog_max_blocks(o, V, 4, o.rows_per_wave) : 0);
 }
 
-extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
-                            const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
-                            float lr, int mode, void *stream) {
+extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks,
+                            int64_t P, int L, const uint64_t *seeds, int window, int negative,
+                            const uint32_t *table, uint64_t T, float lr, float alpha, int mode,
+                            void *stream) {
+    return come_sgns_o2_ex(node, ctx, V, d, walks, P, L, seeds, window, negative, table, T, lr,
+                           alpha, mode, nullptr, nullptr, stream);
+}
+
+extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
+                               const uint64_t *seeds, int negative, const uint32_t *table,
+                               uint64_t T, float lr, int mode, const uint32_t *hot_rows,
+                               const come_launch_opts *opts, void *stream) {
+    const come_launch_opts o = opts ? *opts : current_opts();
     int packed = 0;
     int rc = check_common(V, d, negative, table, T, mode, packed);
     if (rc) return rc;
@@ -206,12 +186,20 @@ extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges,
         return set_error(COME_E_INVALID, "O1 supports negative <= 32 (got %d)", negative);
     if (!aligned_for(node, d))
         return set_error(COME_E_INVALID, "node must be 16-byte aligned for d=%d", d);
-    O1Args a{node, edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed};
+    O1Args a{node,           edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed,
+             mode == COME_MODE_HOGWILD ? hot_rows : nullptr};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
-    return launch(ks.o1[full][maxn_index(negative)], &a, E, mode, 4,
-                  g_opt_o1_blocks_per_cu > 0 ? g_opt_o1_blocks_per_cu : 6, 0, stream,
-                  mode == COME_MODE_HOGWILD ? hog_max_blocks(V, 4, g_opt_o1_rows_per_wave) : 0);
+    return launch(o, ks.o1[full][maxn_index(negative)], &a, E, mode, 4,
+                  o.o1_blocks_per_cu > 0 ? o.o1_blocks_per_cu : 6, 0, stream,
+                  mode == COME_MODE_HOGWILD ? hog_max_blocks(o, V, 4, o.o1_rows_per_wave) : 0);
+}
+
+extern "C" int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
+                            const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
+                            float lr, int mode, void *stream) {
+    return come_sgns_o1_ex(node, V, d, edges, E, seeds, negative, table, T, lr, mode, nullptr,
+                           nullptr, stream);
 }
 
 // One wavefront per 64-slot word: lane i loads slot 64w + i (one coalesced 256-B read), the
@@ -266,31 +254,4 @@ extern "C" int come_upload_exp_table(const float *host1000) {
         if (rc) return rc;
     }
     return COME_OK;
-}
-
-extern "C" int come_set_option(const char *name, int value) {
-    if (!name) return set_error(COME_E_INVALID, "null option name");
-    struct {
-        const char *k;
-        int *v;
-    } opts[] = {{"o2_kernel", &g_opt_o2_kernel},
-                {"o2_blocks_per_cu", &g_opt_o2_blocks_per_cu},
-                {"o2_plain_writeback", &g_opt_o2_plain_writeback},
-                {"o2_waves_per_block", &g_opt_o2_waves_per_block},
-                {"o2_static", &g_opt_o2_static},
-                {"o2_pair_atomics", &g_opt_o2_pair_atomics},
-                {"rows_per_wave", &g_opt_rows_per_wave},
-                {"o1_rows_per_wave", &g_opt_o1_rows_per_wave},
-                {"max_waves", &g_opt_max_waves},
-                {"o1_blocks_per_cu", &g_opt_o1_blocks_per_cu},
-                {"resident_cap", &g_opt_resident_cap},
-                {"community_async", &g_comm_async},
-                {"gmm_cov_async", &g_cov_async},
-                {"walk_staged", &g_walk_staged}};
-    for (auto &o : opts)
-        if (!strcmp(o.k, name)) {
-            *o.v = value;
-            return COME_OK;
-        }
-    return set_error(COME_E_INVALID, "unknown option '%s'", name);
 }

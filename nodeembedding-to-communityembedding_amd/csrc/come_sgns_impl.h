@@ -49,6 +49,39 @@ __device__ inline LcgLane lcg_lane_constants(int k) {
 
 __device__ inline uint64_t lcg_next(uint64_t s) { return (s * kLcgMul + kLcgAdd) & kLcgMask; }
 
+// The 64 lanes' jump-ahead constants as a table in constant memory: a kernel short of registers
+// reads its lane's pair when it refills a batch of draws (every 64 draws) instead of holding
+// four VGPRs for the whole kernel.
+struct LcgTable {
+    uint64_t a[64], c[64];
+};
+constexpr LcgTable make_lcg_table() {
+    LcgTable t{};
+    uint64_t a = 1, c = 0;
+    for (int k = 0; k < 64; ++k) {
+        t.a[k] = a;
+        t.c[k] = c;
+        a = (a * kLcgMul) & kLcgMask;
+        c = (c * kLcgMul + kLcgAdd) & kLcgMask;
+    }
+    return t;
+}
+static __constant__ LcgTable c_lcg = make_lcg_table();
+constexpr LcgTable kLcgHost = make_lcg_table();
+// state 64 draws after s, for any lane: A^64 s + C_64 (wave-uniform, scalar)
+constexpr uint64_t kLcgA64 = (kLcgHost.a[63] * kLcgMul) & kLcgMask;
+constexpr uint64_t kLcgC64 = (kLcgHost.c[63] * kLcgMul + kLcgAdd) & kLcgMask;
+
+struct LcgFromTable {  // same interface as LcgLane, constants read at use
+    int lane;
+};
+__device__ inline uint64_t lcg_state_of(uint64_t base, const LcgLane &lc) {
+    return (lc.a * base + lc.c) & kLcgMask;
+}
+__device__ inline uint64_t lcg_state_of(uint64_t base, const LcgFromTable &lt) {
+    return (c_lcg.a[lt.lane] * base + c_lcg.c[lt.lane]) & kLcgMask;
+}
+
 __device__ inline uint32_t table_slot(uint64_t s, uint64_t m, uint32_t d) {
     const uint32_t x = (uint32_t)(s >> 16);  // < 2^32 because s < 2^48 (pyx:133)
     if (d == 0) return x;                     // T >= 2^32: x % T == x
@@ -110,6 +143,24 @@ struct Row {
             const int e = lane + 64 * i;
             v[i] = (FULL || e < d) ? row[e] : 0.0f;
         }
+    }
+
+    // Agent-scope relaxed loads (global_load ... sc1): bypass this CU's L1, which other CUs'
+    // stores never refresh (MI355X_MICROARCH.md: inter-workgroup visibility), so a row several
+    // wavefronts update is read as last written to L2 / memory.
+    __device__ inline void load_fresh(const float *__restrict__ row, int lane, int d) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const int e = lane + 64 * i;
+            v[i] = (FULL || e < d) ? __hip_atomic_load(row + e, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0.0f;
+        }
+    }
+
+    __device__ inline void load_as(const float *__restrict__ row, int lane, int d, bool fresh) {
+        if (fresh) load_fresh(row, lane, d);
+        else load(row, lane, d);
     }
 
     __device__ inline void store(float *__restrict__ row, int lane, int d) const {
@@ -201,10 +252,20 @@ struct DrawPipe {
     uint64_t base0, base1;
     int used;
 
-    template <class Args>
-    __device__ inline uint32_t gather(uint64_t base, const LcgLane &lc, const Args &a) {
-        const uint64_t s = (lc.a * base + lc.c) & kLcgMask;  // draw base + lane
+    template <class Args, class Lcg>
+    __device__ inline uint32_t gather(uint64_t base, const Lcg &lc, const Args &a) {
+        const uint64_t s = lcg_state_of(base, lc);  // draw base + lane
         return table_value(a, table_slot(s, a.fm.m, a.fm.d));
+    }
+
+    // gather() plus the drawn row's hot bit (a.hot) in bit 31 (rows are < 2^31); a table value
+    // outside [0, V) gets no bit and stays out of range.  The bitmap word is one more dependent
+    // per-lane load, 64 draws ahead of use.
+    template <class Args, class Lcg>
+    __device__ inline uint32_t gather_hot(uint64_t base, const Lcg &lc, const Args &a) {
+        const uint32_t v = gather(base, lc, a);
+        if (a.hot == nullptr || (int64_t)v >= a.V) return v;
+        return v | (((a.hot[v >> 5] >> (v & 31)) & 1u) << 31);
     }
 };
 
@@ -227,10 +288,19 @@ struct O2Args {
     FastMod fm;
     int packed;        // table points to come_pack_table's words
     int64_t *counter;  // work queue: walks are claimed with atomicAdd (nullptr = grid-stride)
-    float *orig;       // HOG, optional: per-wavefront [2w+1][d] entry snapshots of the ring rows
-                       // (node rows then get ONE atomic delta when they leave the window instead
-                       // of one atomic per pair); nullptr = per-pair atomics
+    unsigned long long *upd_count;  // optional: += target row updates applied (come.h
+                                    // o2_update_count); one atomic per walk
+    int fresh;       // direct kernel: rows read with agent-scope loads (bypass the CU's L1)
+    int wb_atomic;   // direct kernel: row updates written as float-atomic deltas (none lost)
+    const uint32_t *hot;  // HOG, optional: bitmap of contended rows (come_hot_rows); their
+                          // updates are float-atomic deltas, their reads are per pair
 };
+
+// Row r is in the hot bitmap (wave-uniform r: one scalar load).
+template <class Args>
+__device__ inline bool is_hot(const Args &a, int r) {
+    return a.hot != nullptr && ((a.hot[(uint32_t)r >> 5] >> (r & 31)) & 1u);
+}
 
 // Next unit of a wavefront: from the launch's work queue (one atomic per unit; a wavefront that
 // starts late -- e.g. its CU was busy with a concurrent RCCL kernel -- simply claims fewer
@@ -243,9 +313,21 @@ __device__ inline int64_t next_unit(int64_t *counter, int64_t cur, int64_t strid
 }
 
 // State 64 draws after `base` (lane 63's state advanced once).
+__device__ inline uint64_t advance64_uniform(uint64_t base) {
+    return (kLcgA64 * base + kLcgC64) & kLcgMask;
+}
 __device__ inline uint64_t advance64(uint64_t base, const LcgLane &lc) {
     const uint64_t s = (lc.a * base + lc.c) & kLcgMask;
     return lcg_next(uniform64(readlane_u64(s, 63)));
+}
+
+template <int VEC, bool FULL>
+__device__ inline void atomic_add_delta(float *__restrict__ row, const Row<VEC, FULL> &cur,
+                                        const Row<VEC, FULL> &orig, int lane, int d) {
+    Row<VEC, FULL> delta;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) delta.v[e] = cur.v[e] - orig.v[e];
+    delta.atomic_add(row, lane, d);
 }
 
 // One O2 pair (pyx:105-151) with the input row `in` and the positive row `pos` already in
@@ -255,7 +337,7 @@ __device__ inline uint64_t advance64(uint64_t base, const LcgLane &lc) {
 template <int VEC, bool FULL, int MAXN>
 __device__ inline void o2_pair(const O2Args &a, DrawBatch &db, const LcgLane &lc, int lane, int ci,
                                Row<VEC, FULL> &pos, bool &pos_upd, Row<VEC, FULL> &in,
-                               Row<VEC, FULL> &work) {
+                               Row<VEC, FULL> &work, int &nupd) {
     using R = Row<VEC, FULL>;
     const int n = a.negative;
     const int d = a.d;
@@ -278,10 +360,13 @@ __device__ inline void o2_pair(const O2Args &a, DrawBatch &db, const LcgLane &lc
     }
     if (n > 0) db.used += n;
 
-    R r[MAXN + 1];
+    R r[MAXN + 1], o[MAXN + 1];
 #pragma unroll
     for (int k = 1; k <= MAXN; ++k)
-        if (valid[k]) r[k].load(a.ctx + (int64_t)t[k] * d, lane, d);
+        if (valid[k]) {
+            r[k].load_as(a.ctx + (int64_t)t[k] * d, lane, d, a.fresh);
+            o[k] = r[k];
+        }
 
     // dots of every target against the (fixed) input row, butterflies interleaved
     float part[MAXN + 1];
@@ -303,6 +388,7 @@ __device__ inline void o2_pair(const O2Args &a, DrawBatch &db, const LcgLane &lc
                 pos.v[e] = __builtin_fmaf(g, in.v[e], pos.v[e]);     // pyx:147
             }
             pos_upd = true;
+            ++nupd;
         }
     }
     bool upd[MAXN + 1];
@@ -337,22 +423,25 @@ __device__ inline void o2_pair(const O2Args &a, DrawBatch &db, const LcgLane &lc
             r[k].v[e] = __builtin_fmaf(g, in.v[e], r[k].v[e]);    // pyx:147
         }
         upd[k] = true;
+        ++nupd;
     }
-    // write back in order, so a repeated row ends with its last version
+    // write back in order, so a repeated row ends with its last version; atomic mode adds the
+    // row's change over the pair once (last updated occurrence minus the value loaded)
 #pragma unroll
-    for (int k = 1; k <= MAXN; ++k)
-        if (upd[k]) r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+    for (int k = 1; k <= MAXN; ++k) {
+        if (!upd[k]) continue;
+        if (!a.wb_atomic && !is_hot(a, t[k])) {
+            r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+            continue;
+        }
+        bool last = true;
+#pragma unroll
+        for (int q = k + 1; q <= MAXN; ++q)
+            if (upd[q] && t[q] == t[k]) last = false;
+        if (last) atomic_add_delta(a.ctx + (int64_t)t[k] * d, r[k], o[k], lane, d);
+    }
 #pragma unroll
     for (int e = 0; e < VEC; ++e) in.v[e] = in.v[e] + work.v[e];  // pyx:149
-}
-
-template <int VEC, bool FULL>
-__device__ inline void atomic_add_delta(float *__restrict__ row, const Row<VEC, FULL> &cur,
-                                        const Row<VEC, FULL> &orig, int lane, int d) {
-    Row<VEC, FULL> delta;
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) delta.v[e] = cur.v[e] - orig.v[e];
-    delta.atomic_add(row, lane, d);
 }
 
 // Direct variant: every pair reads and writes its input and positive rows in HBM.  Used when the
@@ -375,6 +464,7 @@ __global__ void __launch_bounds__(256) k_sgns_o2(O2Args a) {
         db.base = uniform64(a.seeds[p]);
         db.target = 0;
         if (a.negative > 0) draws_fill(db, db.base, lc, a);
+        int nupd = 0;
         for (int i = 0; i < path_len; ++i) {
             const int ci = uniform(idx[i]);
             if (ci < 0 || ci >= a.V) continue;  // codelens[i] == 0 (pyx:495)
@@ -385,15 +475,25 @@ __global__ void __launch_bounds__(256) k_sgns_o2(O2Args a) {
                 const int cj = uniform(idx[j]);
                 if (cj < 0 || cj >= a.V) continue;  // pyx:504
                 R in, pos;
-                in.load(a.node + (int64_t)cj * d, lane, d);
-                pos.load(a.ctx + (int64_t)ci * d, lane, d);
+                in.load_as(a.node + (int64_t)cj * d, lane, d, a.fresh);
+                pos.load_as(a.ctx + (int64_t)ci * d, lane, d, a.fresh);
+                const R pos0 = pos;
                 bool pos_upd = false;
                 R work;
-                o2_pair<VEC, FULL, MAXN>(a, db, lc, lane, ci, pos, pos_upd, in, work);
-                if (pos_upd) pos.store(a.ctx + (int64_t)ci * d, lane, d);
-                in.store(a.node + (int64_t)cj * d, lane, d);
+                o2_pair<VEC, FULL, MAXN>(a, db, lc, lane, ci, pos, pos_upd, in, work, nupd);
+                // in += work and pos's change: at the memory side (float atomics) for contended
+                // rows, plain stores otherwise
+                if (pos_upd) {
+                    if (a.wb_atomic || is_hot(a, ci))
+                        atomic_add_delta(a.ctx + (int64_t)ci * d, pos, pos0, lane, d);
+                    else
+                        pos.store(a.ctx + (int64_t)ci * d, lane, d);
+                }
+                if (a.wb_atomic || is_hot(a, cj)) work.atomic_add(a.node + (int64_t)cj * d, lane, d);
+                else in.store(a.node + (int64_t)cj * d, lane, d);
             }
         }
+        if (a.upd_count && lane == 0 && nupd) atomicAdd(a.upd_count, (unsigned long long)nupd);
     }
 }
 
@@ -416,13 +516,13 @@ __global__ void __launch_bounds__(256) k_sgns_o2(O2Args a) {
 //    it is used is replaced by the register copy (forwarding), so sequential order is preserved
 //    bit for bit.  Prefetch loads are unconditional (out-of-range targets read row 0 and are
 //    discarded) so the compiler's vmcnt waits stay counted, never vmcnt(0).
-// Write-back.  SEQ (one wavefront, the parity mode): plain stores -- the positive once per center,
-// a node row when its last alias leaves the window.  HOG (all walks in flight): every pair adds
-// its `work` to the node row with float atomics and every center adds its positive row's change
-// (cur - orig), so a row several wavefronts hold at once (a hub) loses none of their updates; the
-// LDS / register copies are the wavefront's own Hogwild view.  Negative rows are read-modify-
-// written per pair with plain loads and stores in both modes, as the reference's saxpy does.
-template <int VEC, bool FULL, int MAXN, bool HOG>
+// Write-back: plain stores -- the positive once per center, a node row when its last alias leaves
+// the window, negative rows per pair.
+// This is the SEQUENTIAL-mode kernel (one wavefront, the parity anchor).  Its caching is exact
+// only when no other wavefront touches the cached rows: for Hogwild, caching node rows for a
+// window trains measurably worse on graphs with hubs (tests/test_gpu_tierc.py), so Hogwild runs
+// k_sgns_o2_stream.
+template <int VEC, bool FULL, int MAXN>
 __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
     using R = Row<VEC, FULL>;
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -499,6 +599,7 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
         };
         fetch_next();
 
+        int nupd = 0;  // target row updates of this walk (wave-uniform)
         // ---- ring (LDS rows) + ids (one per lane) ----
         int ids = -1;  // lane s: node row held by ring slot s
         auto id_of = [&](int s) { return __builtin_amdgcn_readlane(ids, s); };
@@ -506,35 +607,20 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
             return __ballot(lane < RS && lane != except && ids == id);
         };
         auto set_id = [&](int s, int id) { ids = lane == s ? id : ids; };
-        float *orig = HOG && a.orig ? a.orig + gw * (int64_t)RS * d : nullptr;
-        auto write_back = [&](int s, int id) {  // the last holder of a node row writes it back
+        auto write_back = [&](int s, int id) {  // the last holder of a node row stores it
             if (alias_mask(id, s) != 0) return;
-            if (!HOG) {  // SEQ: plain store
-                R row;
-                row.load(ring + s * d, lane, d);
-                row.store(a.node + (int64_t)id * d, lane, d);
-            } else if (orig) {  // HOG, delta-at-exit: node[id] += cur - entry snapshot
-                R row, o;
-                row.load(ring + s * d, lane, d);
-                o.load(orig + s * d, lane, d);
-                atomic_add_delta(a.node + (int64_t)id * d, row, o, lane, d);
-            }
+            R row;
+            row.load(ring + s * d, lane, d);
+            row.store(a.node + (int64_t)id * d, lane, d);
         };
         auto enter_row = [&](int s, int id, const R &fetched) {  // fetched: node[id] loaded earlier
             const uint64_t m = alias_mask(id, s);
             if (m) {
                 R row;
-                const int src = __builtin_ctzll(m);
-                row.load(ring + src * d, lane, d);
+                row.load(ring + __builtin_ctzll(m) * d, lane, d);
                 row.store(ring + s * d, lane, d);
-                if (orig) {  // every alias carries the snapshot of the id's first entry
-                    R o;
-                    o.load(orig + src * d, lane, d);
-                    o.store(orig + s * d, lane, d);
-                }
             } else {
                 fetched.store(ring + s * d, lane, d);
-                if (orig) fetched.store(orig + s * d, lane, d);
             }
             set_id(s, id);
         };
@@ -582,8 +668,6 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
             ent_n.load(a.node + (int64_t)(ent_n_id >= 0 ? ent_n_id : 0) * d, lane, d);
 
             if (ci >= 0) {  // codelens[i] != 0 (pyx:495)
-                R pos0;
-                if (HOG) pos0 = pos;
                 bool pos_upd = false;
                 const int j0 = i - w < 0 ? 0 : i - w;
                 const int j1 = i + w + 1 > path_len ? path_len : i + w + 1;
@@ -628,6 +712,7 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
                                 pos.v[e] = __builtin_fmaf(g, in.v[e], pos.v[e]);     // pyx:147
                             }
                             pos_upd = true;
+                            ++nupd;
                         }
                     }
                     bool upd[MAXN + 1];
@@ -660,6 +745,7 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
                             r[k].v[e] = __builtin_fmaf(g, in.v[e], r[k].v[e]);    // pyx:147
                         }
                         upd[k] = true;
+                        ++nupd;
                     }
 #pragma unroll
                     for (int k = 1; k <= MAXN; ++k) {
@@ -673,7 +759,6 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
                     }
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) in.v[e] = in.v[e] + work.v[e];  // pyx:149
-                    if (HOG && !orig) work.atomic_add(a.node + (int64_t)cj * d, lane, d);
                     uint64_t m = alias_mask(cj, -1);  // the slot and every alias of it
                     while (m) {
                         const int rr = __builtin_ctzll(m);
@@ -682,8 +767,7 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
                     }
                 }
                 if (pos_upd) {
-                    if (HOG) atomic_add_delta(a.ctx + (int64_t)ci * d, pos, pos0, lane, d);
-                    else pos.store(a.ctx + (int64_t)ci * d, lane, d);
+                    pos.store(a.ctx + (int64_t)ci * d, lane, d);
 #pragma unroll
                     for (int q = 1; q <= MAXN; ++q)
                         if (tn[q] == ci) rn[q] = pos;  // prefetched before this write-back
@@ -700,6 +784,297 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
             if (id >= 0) write_back(s, id);
             set_id(s, -1);
         }
+        if (a.upd_count && lane == 0 && nupd) atomicAdd(a.upd_count, (unsigned long long)nupd);
+    }
+}
+
+// Streaming Hogwild variant (COME_MODE_HOGWILD; the product's Hogwild mode).
+//
+// Semantics per pair are the reference thread's (pyx:128-149): the input row, the positive row and
+// the negative rows are read from memory for the pair and written back after it -- nothing is
+// cached across pairs except a cold center's positive row, held for that center's 2w pairs (no
+// negative of those pairs can be that row, pyx:135).  Rows are split by contention (a.hot,
+// come_hot_rows): cold rows are written back with plain stores (few other wavefronts touch them
+// while the pair runs), hot rows (hubs) with float-atomic deltas at the memory side (none of the
+// many concurrent updates lost).  Measured against the sequential oracle on a power-law graph
+// (tests/test_gpu_tierc.py): caching node rows for a window (the ring kernel's traffic cut) and
+// writing them back later trains 3.6-6% worse, plain stores for hubs 1.8% worse, this form within
+// 1% (the 1% bar of SURVEY.md §8c tier C).
+// Latency hiding as in the ring kernel, one pair ahead: the next pair's input row, its positive
+// (when the center changes or is hot), its negative rows and the hot bits of its rows are in
+// flight while the current pair computes; the next 64 table draws (with their hot bits) while the
+// current 64 are consumed.  A prefetched copy of a row the current pair then updates receives
+// that update additively (copy + delta), so it keeps both the other wavefronts' updates it was
+// loaded with and this wavefront's own.
+// Wavefronts per SIMD the stream kernel is compiled for: the kernel is latency-bound (one pair of
+// loads in flight per wavefront), so at d <= 128, n <= 5 it is held to 64 VGPRs for 8 waves per
+// SIMD (a 32-byte spill): 108 vs 119 ms per C3 launch at the 7 waves 70 VGPRs would give
+// (profiles/r02_ab_stream_occupancy.txt).  Wider rows / more negatives keep their natural size.
+template <int VEC, int MAXN>
+constexpr int stream_waves_per_eu() { return (VEC <= 2 && MAXN <= 5) ? 8 : 1; }
+
+template <int VEC, bool FULL, int MAXN>
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu(stream_waves_per_eu<VEC, MAXN>())))
+    k_sgns_o2_stream(O2Args a) {
+    using R = Row<VEC, FULL>;
+    const int lane = threadIdx.x & 63;
+    const int64_t waves_per_block = blockDim.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * waves_per_block;
+    const LcgFromTable lc{lane};
+    const int d = a.d;
+    const int w = a.window;  // <= 31 (launcher): lookups never fall behind the index window
+    const int n = a.negative;
+    const int path_len = a.L < kMaxSentenceLen ? a.L : kMaxSentenceLen;  // pyx:480
+    auto valid_row = [&](int r) { return r >= 0 && r < a.V; };
+    constexpr uint32_t kHotBit = 0x80000000u;
+
+    for (int64_t p = a.counter ? next_unit(a.counter, 0, 0, lane) : gw; p < a.P;
+         p = next_unit(a.counter, p, nwaves, lane)) {
+        const int32_t *__restrict__ walk = a.walks + p * (int64_t)a.L;
+        // ---- walk indices: positions [wbase, wbase + 128) in two VGPR chunks, slid forward.
+        // Each lane holds one position's row with its hot bit in bit 31 (gathered when the chunk
+        // is loaded, 64 positions ahead of use); -1 = None / past the end.
+        auto chunk = [&](int q0) {
+            const int q = q0 + lane;
+            int v = q < path_len ? walk[q] : -1;
+            if (!valid_row(v)) return -1;
+            if (a.hot != nullptr && ((a.hot[(uint32_t)v >> 5] >> (v & 31)) & 1u))
+                v = (int)((uint32_t)v | kHotBit);
+            return v;
+        };
+        int wbase = 0;
+        int c0 = chunk(0);
+        int c1 = chunk(64);
+        auto raw_at = [&](int q) {  // encoded row of walk position q
+            if (q >= path_len) return -1;
+            while (q - wbase >= 128) {  // positions behind q - 2w are never asked for again
+                wbase += 64;
+                c0 = c1;
+                c1 = chunk(wbase + 64);
+            }
+            const int off = q - wbase;
+            return off < 64 ? __builtin_amdgcn_readlane(c0, off)
+                            : __builtin_amdgcn_readlane(c1, off - 64);
+        };
+        // ---- pairs in the reference order (pyx:494-508): center i ascending, j ascending ----
+        int it_i = 0, it_j = -1;
+        auto next_pair = [&](int &ci, int &cj, int &pi, bool &hi, bool &hj) -> bool {
+            for (;;) {
+                if (it_i >= path_len) return false;
+                const int i = it_i;
+                const int j0 = i - w < 0 ? 0 : i - w;
+                const int j1 = i + w + 1 > path_len ? path_len : i + w + 1;
+                if (it_j < j0) it_j = j0;
+                const int rci = raw_at(i);
+                if (rci == -1 || it_j >= j1) {  // codelens[i] == 0, or the center is done
+                    ++it_i;
+                    it_j = -1;
+                    continue;
+                }
+                const int j = it_j++;
+                if (j == i) continue;
+                const int rcj = raw_at(j);
+                if (rcj == -1) continue;  // pyx:504
+                ci = (int)((uint32_t)rci & ~kHotBit);
+                cj = (int)((uint32_t)rcj & ~kHotBit);
+                hi = ((uint32_t)rci & kHotBit) != 0;
+                hj = ((uint32_t)rcj & kHotBit) != 0;
+                pi = i;
+                return true;
+            }
+        };
+        // ---- draws (hot bit in bit 31) ----
+        DrawPipe dp;
+        dp.used = 0;
+        dp.base0 = uniform64(a.seeds[p]);
+        dp.t0 = dp.t1 = 0;
+        if (n > 0) {
+            dp.t0 = dp.gather_hot(dp.base0, lc, a);
+            dp.base1 = advance64_uniform(dp.base0);
+            dp.t1 = dp.gather_hot(dp.base1, lc, a);
+        }
+        auto take = [&](int k) -> uint32_t {
+            const int q = dp.used + k;
+            return q < 64 ? readlane_u32(dp.t0, q) : readlane_u32(dp.t1, q - 64);
+        };
+        auto advance = [&]() {
+            if (n == 0) return;
+            dp.used += n;
+            if (dp.used >= 64) {
+                dp.used -= 64;
+                dp.t0 = dp.t1;
+                dp.base0 = dp.base1;
+                dp.base1 = advance64_uniform(dp.base1);
+                dp.t1 = dp.gather_hot(dp.base1, lc, a);
+            }
+        };
+        // ---- the next pair: ids, hot bits, rows in flight ----
+        int nci = -1, ncj = -1, npi = -1;
+        bool nhi = false, nhj = false;
+        int tn[MAXN + 1];
+        bool tnh[MAXN + 1];
+        R in_n, pos_n, rn[MAXN + 1];
+        int prev_i = -1;  // center of the pair just done
+        auto prefetch = [&](bool need_pos) {  // rows of the pair next_pair() just produced
+            in_n.load(a.node + (int64_t)ncj * d, lane, d);
+            if (need_pos) pos_n.load(a.ctx + (int64_t)nci * d, lane, d);
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                const uint32_t raw = k <= n ? take(k - 1) : 0xFFFFFFFFu;
+                tn[k] = (int)(raw & ~kHotBit);
+                tnh[k] = (raw & kHotBit) != 0;
+                if (k > n) tn[k] = -1;
+                rn[k].load(a.ctx + (int64_t)(valid_row(tn[k]) ? tn[k] : 0) * d, lane, d);
+            }
+        };
+        bool have = next_pair(nci, ncj, npi, nhi, nhj);
+        if (have) prefetch(true);
+        int nupd = 0;
+        R pos;  // the current center's positive (carried across the center's pairs while cold)
+        bool pos_upd = false;
+
+        while (have) {
+            // ---- the next pair becomes the current one ----
+            const int ci = nci, cj = ncj, ic = npi;
+            const bool hot_ci = nhi, hot_cj = nhj;
+            R in = in_n;
+            int t[MAXN + 1];
+            bool th[MAXN + 1];
+            R r[MAXN + 1];
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                t[k] = tn[k];
+                th[k] = tnh[k];
+                r[k] = rn[k];
+            }
+            const bool new_center = ic != prev_i;
+            if (new_center || hot_ci) pos = pos_n;  // a hot positive is re-read for every pair
+            if (new_center) pos_upd = false;
+            prev_i = ic;
+            // ---- put the pair after it in flight ----
+            advance();
+            have = next_pair(nci, ncj, npi, nhi, nhj);
+            if (have) prefetch(npi != ic || nhi);
+
+            // ---- the pair (pyx:128-149) ----
+            bool valid[MAXN + 1];
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k)
+                valid[k] = k <= n && t[k] != ci && valid_row(t[k]);  // pyx:135
+            float part[MAXN + 1];
+            part[0] = lane_partial(in, pos);
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) part[k] = lane_partial(in, r[k]);
+            wave_sum_n(part, n + 1);
+            R work;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) work.v[e] = 0.0f;
+            float gpos = 0.0f;  // this pair's g of the positive (0 = skipped)
+            {
+                float sig;
+                if (sigmoid_ref(uniformf(part[0]), &sig)) {
+                    const float g = ((1.0f - sig) * a.lr) * a.alpha;  // pyx:144
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {
+                        work.v[e] = __builtin_fmaf(g, pos.v[e], work.v[e]);  // pyx:146
+                        pos.v[e] = __builtin_fmaf(g, in.v[e], pos.v[e]);     // pyx:147
+                    }
+                    pos_upd = true;
+                    gpos = g;
+                    ++nupd;
+                }
+            }
+            bool upd[MAXN + 1];
+            float gk[MAXN + 1];
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                upd[k] = false;
+                gk[k] = 0.0f;
+                if (!valid[k]) continue;
+                float f = part[k];
+                int prev = -1;  // latest earlier occurrence of the same negative row
+#pragma unroll
+                for (int q = 1; q < k; ++q)
+                    if (valid[q] && t[q] == t[k]) prev = q;
+                if (prev >= 0) {
+#pragma unroll
+                    for (int q = 1; q < k; ++q) {
+                        if (q == prev) {
+                            r[k] = r[q];
+                            f = upd[q] ? wave_sum(lane_partial(in, r[k])) : part[q];
+                        }
+                    }
+                }
+                f = uniformf(f);
+                part[k] = f;
+                float sig;
+                if (!sigmoid_ref(f, &sig)) continue;  // pyx:141-142
+                const float g = ((0.0f - sig) * a.lr) * a.alpha;  // pyx:144, label 0
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) {
+                    work.v[e] = __builtin_fmaf(g, r[k].v[e], work.v[e]);  // pyx:146
+                    r[k].v[e] = __builtin_fmaf(g, in.v[e], r[k].v[e]);    // pyx:147
+                }
+                upd[k] = true;
+                gk[k] = g;
+                ++nupd;
+            }
+            // ---- write-back: negatives (in order; a repeated row ends with its last version) ----
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                if (!upd[k]) continue;
+                R dlt;  // this occurrence's change, g * in
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) dlt.v[e] = gk[k] * in.v[e];
+                if (th[k]) dlt.atomic_add(a.ctx + (int64_t)t[k] * d, lane, d);
+                else r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+#pragma unroll
+                for (int q = 1; q <= MAXN; ++q)
+                    if (tn[q] == t[k])
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) rn[q].v[e] += dlt.v[e];
+                if (have && nci == t[k] && (npi != ic || nhi))
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) pos_n.v[e] += dlt.v[e];
+            }
+            // ---- the positive: hot -> this pair's change, g * in, now (memory side) and into the
+            // prefetched copies; cold -> stored once when the center ends, and its final value
+            // replaces prefetched copies (no other wavefront updates a cold row meanwhile)
+            if (hot_ci && gpos != 0.0f) {
+                R pdl;
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) pdl.v[e] = gpos * in.v[e];
+                pdl.atomic_add(a.ctx + (int64_t)ci * d, lane, d);
+#pragma unroll
+                for (int q = 1; q <= MAXN; ++q)
+                    if (tn[q] == ci)
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) rn[q].v[e] += pdl.v[e];
+                if (have && nci == ci)
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) pos_n.v[e] += pdl.v[e];
+            } else if (!hot_ci && pos_upd && (!have || npi != ic)) {
+                pos.store(a.ctx + (int64_t)ci * d, lane, d);
+#pragma unroll
+                for (int q = 1; q <= MAXN; ++q)
+                    if (tn[q] == ci) rn[q] = pos;
+                if (have && nci == ci) pos_n = pos;
+            }
+            // ---- the input row: in += work (pyx:149) ----
+            if (hot_cj) {
+                work.atomic_add(a.node + (int64_t)cj * d, lane, d);
+            } else {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) in.v[e] = in.v[e] + work.v[e];
+                in.store(a.node + (int64_t)cj * d, lane, d);
+            }
+            if (have && ncj == cj)
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) in_n.v[e] += work.v[e];
+        }
+        if (a.upd_count && lane == 0 && nupd) atomicAdd(a.upd_count, (unsigned long long)nupd);
     }
 }
 
@@ -716,6 +1091,7 @@ struct O1Args {
     float lr;
     FastMod fm;
     int packed;
+    const uint32_t *hot;  // HOG, optional: contended rows (come_hot_rows), updated atomically
 };
 
 template <int VEC, bool FULL, int MAXN>
@@ -763,6 +1139,7 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
         R in1, in2;
         in1.load(a.node + (int64_t)u * d, lane, d);
         if (v != u) in2.load(a.node + (int64_t)v * d, lane, d);
+        const bool hot_u = is_hot(a, u), hot_v = is_hot(a, v);
         R r1[MAXN + 1], r2[MAXN + 1];
 #pragma unroll
         for (int k = 1; k <= MAXN; ++k) {
@@ -791,7 +1168,8 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
             }
 #pragma unroll
             for (int q = 0; q < VEC; ++q) in1.v[q] = in1.v[q] + work.v[q];  // pyx:247
-            in1.store(a.node + (int64_t)u * d, lane, d);
+            if (hot_u) work.atomic_add(a.node + (int64_t)u * d, lane, d);
+            else in1.store(a.node + (int64_t)u * d, lane, d);
         }
         // pair 2: positive = node[u] as pair 1 left it; self-loop: the input is that row too.
         r2[0] = in1;
@@ -815,7 +1193,8 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
             }
 #pragma unroll
             for (int q = 0; q < VEC; ++q) in2.v[q] = in2.v[q] + work.v[q];
-            in2.store(a.node + (int64_t)v * d, lane, d);
+            if (hot_v) work.atomic_add(a.node + (int64_t)v * d, lane, d);
+            else in2.store(a.node + (int64_t)v * d, lane, d);
         }
     }
 }
@@ -823,8 +1202,9 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
 // Kernel entry addresses per instantiation (defined in come_sgns_vec{1,2,4,8}.hip so the
 // instantiations compile in parallel).
 struct KernelSet {
-    void *o2_direct[2][3];   // [FULL][maxn idx]
-    void *o2_ring[2][3][2];  // [FULL][maxn idx][HOG]
+    void *o2_direct[2][3];  // [FULL][maxn idx]
+    void *o2_ring[2][3];    // sequential mode
+    void *o2_stream[2][3];  // Hogwild mode
     void *o1[2][3];
 };
 #define COME_DECLARE_VEC(V) \

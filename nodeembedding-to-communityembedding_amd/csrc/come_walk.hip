@@ -141,8 +141,6 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_random_walks_staged(WalkArgs a) 
 
 using namespace come;
 
-int come::g_walk_staged = 1;  // come_set_option("walk_staged", 0): direct per-lane row stores
-
 extern "C" int come_random_walks(const int64_t *rowptr, const int32_t *col, int64_t V,
                                  const int32_t *starts, int64_t P, int L, float alpha,
                                  uint64_t seed, int64_t walk_offset, const int32_t *emit,
@@ -162,9 +160,10 @@ extern "C" int come_random_walks(const int64_t *rowptr, const int32_t *col, int6
     if (blocks > INT32_MAX) return set_error(COME_E_INVALID, "too many walks in one launch");
     void *kargs[] = {&a};
     // walk_staged: 1 = 16-step slices (default), 2 = 8, 3 = 32 (A/B), 0 = direct stores
-    const void *k = g_walk_staged == 0   ? (const void *)k_random_walks
-                    : g_walk_staged == 2 ? (const void *)k_random_walks_staged<8>
-                    : g_walk_staged == 3 ? (const void *)k_random_walks_staged<32>
+    const int staged = current_opts().walk_staged;
+    const void *k = staged == 0   ? (const void *)k_random_walks
+                    : staged == 2 ? (const void *)k_random_walks_staged<8>
+                    : staged == 3 ? (const void *)k_random_walks_staged<32>
                                          : (const void *)k_random_walks_staged<16>;
     hipError_t e = hipLaunchKernel(k, dim3((unsigned)blocks), dim3(WALK_BLOCK), kargs, 0,
                                    (hipStream_t)stream);

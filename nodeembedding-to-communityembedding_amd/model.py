@@ -141,6 +141,20 @@ class Model(object):
             from .training_sdg_inner import pack_table
             self.table_packed = pack_table(self.table)
 
+    def hot_rows(self, share=None):
+        """Bitmap (CUDA) of the contended rows for Hogwild launches: rows holding at least `share`
+        of the negative table (default training_sdg_inner.DEFAULT_HOT_P) -- see come_hot.hip.
+        Cached per share; None when the tables are not on a GPU."""
+        from . import training_sdg_inner as tsi
+        share = tsi.DEFAULT_HOT_P if share is None else float(share)
+        if not getattr(self.table, "is_cuda", False) or share <= 0:
+            return None
+        cache = self.__dict__.setdefault("_hot_cache", {})
+        if share not in cache:
+            cache[share] = tsi.hot_rows(self.table, self.vocab_size,
+                                        max(1, int(share * self.table_size)))
+        return cache[share]
+
     def negative_table(self):
         """What the trainers pass to the kernels: the plain uint32 table, or its exact packed
         form when ``use_packed_table`` is set (same draws; measured 1% slower at C3, where the
@@ -159,7 +173,7 @@ class Model(object):
         os.makedirs(path, exist_ok=True)
         state = {}
         for k, v in self.__dict__.items():
-            if k in ("_vocab", "table_packed"):
+            if k in ("_vocab", "table_packed", "_hot_cache"):
                 continue
             if isinstance(v, np.ndarray):
                 state["np:" + k] = torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32

@@ -49,11 +49,12 @@ class Node2Vec(object):
         dev = model.node_embedding.device
         ed = torch.from_numpy(rows).to(dev)
         mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
+        hot = None if self.deterministic else model.hot_rows()
         for _ in range(int(iter)):
             seeds = tsi.draw_seeds(rows.shape[0])
             sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
             tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.negative_table(),
-                        self.lr, mode)
+                        self.lr, mode, hot=hot)
         torch.cuda.synchronize(dev)
         pairs = 2 * int((rows >= 0).all(axis=1).sum()) * int(iter)
         elapsed = time.time() - start

@@ -90,13 +90,47 @@ def _table_args(table):
     return ptr(table), table.numel(), 0
 
 
-def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mode=MODE_HOGWILD):
+def _opts_arg(opts, update_count=None):
+    """ctypes argument for the *_ex entry points: None (process-wide options) or a LaunchOpts."""
+    import ctypes
+    if opts is None and update_count is None:
+        return None
+    if update_count is not None:
+        import torch
+        _require_cuda(update_count, "update_count", torch.int64)
+    o = _lib.launch_opts(update_count, **(opts or {}))
+    return ctypes.byref(o)
+
+
+# Rows holding at least this share of the negative table are "hot" (contended in Hogwild mode,
+# see come_hot.hip): measured on C3's shape (tests/test_gpu_tierc.py, scripts/diag_tierc.py).
+DEFAULT_HOT_P = 1e-5
+
+
+def hot_rows(table, V, min_count):
+    """Bitmap (CUDA int32 tensor [ceil(V/32)]) of the rows holding >= min_count slots of the
+    negative table `table` (CUDA uint32-as-int32 [T]): come_hot_rows."""
+    import torch
+    _require_cuda(table, "table", torch.int32)
+    counts = torch.empty(int(V), dtype=torch.int32, device=table.device)
+    bits = torch.empty((int(V) + 31) // 32, dtype=torch.int32, device=table.device)
+    check(_lib.lib().come_hot_rows(ptr(table), table.numel(), int(V), int(min_count), ptr(counts),
+                                   ptr(bits), stream_handle(table.device)), "come_hot_rows")
+    return bits
+
+
+def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mode=MODE_HOGWILD,
+            opts=None, update_count=None, hot=None):
     """Batched train_o2: every walk of ``walks`` [P, L] (int32 rows, -1 = None) in one launch.
 
     node, ctx: float32 CUDA tensors [V, d], updated in place.  seeds: uint64 (stored as int64)
     CUDA tensor [P].  table: uint32 (stored as int32) CUDA tensor [T].  mode: MODE_HOGWILD (all
     walks in flight, one wavefront each) or MODE_SEQUENTIAL (walks in order: workers=1).  table
-    may also be a PackedTable (same draws, 16x less table traffic)."""
+    may also be a PackedTable (same draws, 16x less table traffic).  opts: per-call launch
+    options (dict of come_launch_opts fields, see include/come.h); update_count: CUDA int64
+    tensor [1] that the launch adds its number of applied target-row updates to; hot: the
+    contended-row bitmap of hot_rows() (Hogwild mode: those rows are read per pair and updated
+    with float atomics)."""
     import torch
     _require_cuda(node, "node", torch.float32)
     _require_cuda(ctx, "ctx", torch.float32)
@@ -110,15 +144,18 @@ def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mod
     if walks.shape[1] > MAX_SENTENCE_LEN:  # pyx:480 truncates silently; so do we
         walks = walks[:, :MAX_SENTENCE_LEN].contiguous()
     V, d = node.shape
-    rc = _lib.lib().come_sgns_o2(ptr(node), ptr(ctx), V, d, ptr(walks), walks.shape[0],
-                                 walks.shape[1], ptr(seeds), int(window), int(negative),
-                                 tp, T, float(lr), float(alpha), int(mode) | flag,
-                                 stream_handle(node.device))
+    rc = _lib.lib().come_sgns_o2_ex(ptr(node), ptr(ctx), V, d, ptr(walks), walks.shape[0],
+                                    walks.shape[1], ptr(seeds), int(window), int(negative),
+                                    tp, T, float(lr), float(alpha), int(mode) | flag,
+                                    None if hot is None else ptr(hot),
+                                    _opts_arg(opts, update_count), stream_handle(node.device))
     check(rc, "come_sgns_o2")
 
 
-def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD):
-    """Batched train_o1 over ``edges`` [E, 2] (int32 rows) in one launch; node updated in place."""
+def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD, opts=None, hot=None):
+    """Batched train_o1 over ``edges`` [E, 2] (int32 rows) in one launch; node updated in place.
+    opts: per-call launch options (dict of come_launch_opts fields); hot: contended-row bitmap
+    (hot_rows(); Hogwild: updates of those rows are float-atomic deltas)."""
     import torch
     _require_cuda(node, "node", torch.float32)
     _require_cuda(edges, "edges", torch.int32)
@@ -127,9 +164,10 @@ def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD):
     if edges.dim() != 2 or edges.shape[1] != 2 or seeds.shape != (edges.shape[0],):
         raise ValueError("edges must be [E, 2] and seeds [E]")
     V, d = node.shape
-    rc = _lib.lib().come_sgns_o1(ptr(node), V, d, ptr(edges), edges.shape[0], ptr(seeds),
-                                 int(negative), tp, T, float(lr), int(mode) | flag,
-                                 stream_handle(node.device))
+    rc = _lib.lib().come_sgns_o1_ex(ptr(node), V, d, ptr(edges), edges.shape[0], ptr(seeds),
+                                    int(negative), tp, T, float(lr), int(mode) | flag,
+                                    None if hot is None else ptr(hot), _opts_arg(opts),
+                                    stream_handle(node.device))
     check(rc, "come_sgns_o1")
 
 

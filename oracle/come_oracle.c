@@ -44,6 +44,11 @@ static int exp_table_ready = 0;
  * whose result could flip with a 1-ulp change of a dot product (SURVEY.md §8c tier A). */
 static double g_min_margin = 1e30;
 void oracle_reset_margin(void) { g_min_margin = 1e30; }
+/* Target-row updates applied since the last reset (targets that passed the +-6 skip): the
+ * quantity the GPU kernels count into come_launch_opts.o2_update_count. */
+static int64_t g_updates = 0;
+void oracle_reset_updates(void) { g_updates = 0; }
+int64_t oracle_updates(void) { return g_updates; }
 double oracle_min_margin(void) { return g_min_margin; }
 static inline void note_margin(float f) {
     double x = ((double)f + 6.0) * 83.0;
@@ -68,13 +73,15 @@ void oracle_exp_table(float *out) {
 /* pyx:134: next_random = (next_random * 25214903917 + 11) & (2^48-1) */
 uint64_t oracle_lcg_next(uint64_t s) { return (s * LCG_MUL + LCG_ADD) & LCG_MASK; }
 
-static float dot_ref(const float *a, const float *b, int d) {
+#define HOT static inline __attribute__((always_inline))
+
+HOT float dot_ref(const float *a, const float *b, int d) {
     double s = 0.0;
     for (int i = 0; i < d; ++i) s += (double)a[i] * (double)b[i];
     return (float)s;
 }
 
-static float dot_wave64(const float *a, const float *b, int d) {
+HOT float dot_wave64(const float *a, const float *b, int d) {
     float lane[64];
     int vec = (d + 63) / 64;
     for (int l = 0; l < 64; ++l) {
@@ -93,13 +100,13 @@ static float dot_wave64(const float *a, const float *b, int d) {
     return lane[0];
 }
 
-static inline float dotp(const float *a, const float *b, int d, int mode) {
+HOT float dotp(const float *a, const float *b, int d, int mode) {
     return mode == COME_DOT_WAVE64 ? dot_wave64(a, b, d) : dot_ref(a, b, d);
 }
 
 /* One pair, pyx:105-151 (o2=1, fast0_o2/fast1_o2) or pyx:205-296 (o2=0, fast0_o1/fast1_o1).
  * in_tab/out_tab are the input and output tables (the same pointer for O1, pyx:444). */
-static uint64_t pair_update(int negative, const uint32_t *table, uint64_t table_len,
+HOT uint64_t pair_update(int negative, const uint32_t *table, uint64_t table_len,
                             float *in_tab, float *out_tab, int size, uint32_t word_index,
                             uint32_t word2_index, float lr, float lam, int o2, float *work,
                             uint64_t next_random, int dot_mode) {
@@ -123,6 +130,7 @@ static uint64_t pair_update(int negative, const uint32_t *table, uint64_t table_
         if (f <= -MAX_EXP || f >= MAX_EXP) continue; /* pyx:141: skip, not clamp */
         /* pyx:143 as generated: EXP_TABLE[(int)((f + 6.0) * 83.0)] in double */
         float s = EXP_TABLE[(int)(((double)f + 6.0) * 83.0)];
+        ++g_updates;
         float g = o2 ? ((label - s) * lr) * lam : (label - s) * lr; /* pyx:144 / :243 */
         for (int i = 0; i < size; ++i) work[i] = fmaf(g, out[i], work[i]);      /* :146 */
         if (o2)
@@ -135,11 +143,9 @@ static uint64_t pair_update(int negative, const uint32_t *table, uint64_t table_
 /* train_o2 (pyx:454-509) over P walks in order.  walks: [P x L] int32 row indices, -1 = None
  * (codelens 0; trailing -1 padding is equivalent to a shorter path).  seeds: per-walk next_random
  * (pyx:477).  Returns the number of pair updates (fast_o2 calls). */
-int64_t oracle_sgns_o2(float *node, float *ctx, int d, const int32_t *walks, int64_t P, int L,
-                       const uint64_t *seeds, int window, int negative, const uint32_t *table,
-                       uint64_t table_len, float lr, float alpha, int dot_mode) {
-    if (!exp_table_ready) oracle_exp_table(NULL);
-    float *work = (float *)malloc(sizeof(float) * (size_t)d);
+HOT int64_t sgns_o2_body(float *node, float *ctx, int d, const int32_t *walks, int64_t P, int L,
+                         const uint64_t *seeds, int window, int negative, const uint32_t *table,
+                         uint64_t table_len, float lr, float alpha, int dot_mode, float *work) {
     int64_t pairs = 0;
     int path_len = L < MAX_SENTENCE_LEN ? L : MAX_SENTENCE_LEN;
     for (int64_t p = 0; p < P; ++p) {
@@ -158,7 +164,6 @@ int64_t oracle_sgns_o2(float *node, float *ctx, int d, const int32_t *walks, int
             }
         }
     }
-    free(work);
     return pairs;
 }
 
@@ -167,11 +172,9 @@ int64_t oracle_sgns_o2(float *node, float *ctx, int d, const int32_t *walks, int
  * positive edge[0] (pyx:447), RNG state carried across both.  Edges with a negative endpoint are
  * skipped (the reference reads uninitialised indexes there: undefined behaviour).  Returns the
  * number of pair updates. */
-int64_t oracle_sgns_o1(float *node, int d, const int32_t *edges, int64_t E,
-                       const uint64_t *seeds, int negative, const uint32_t *table,
-                       uint64_t table_len, float lr, int dot_mode) {
-    if (!exp_table_ready) oracle_exp_table(NULL);
-    float *work = (float *)malloc(sizeof(float) * (size_t)d);
+HOT int64_t sgns_o1_body(float *node, int d, const int32_t *edges, int64_t E,
+                         const uint64_t *seeds, int negative, const uint32_t *table,
+                         uint64_t table_len, float lr, int dot_mode, float *work) {
     int64_t pairs = 0;
     for (int64_t e = 0; e < E; ++e) {
         int32_t u = edges[2 * e], v = edges[2 * e + 1];
@@ -183,6 +186,56 @@ int64_t oracle_sgns_o1(float *node, int d, const int32_t *edges, int64_t E,
                          0.0f, 0, work, nr, dot_mode);
         pairs += 2;
     }
+    return pairs;
+}
+
+/* Each body is built twice: with AVX2 + FMA enabled (explicit fmaf() becomes one vfmadd instead
+ * of a libm call -- the same correctly rounded result, only faster) and for the baseline ISA;
+ * the first call picks one from the CPU.  No reassociation either way (-ffp-contract=off, no
+ * fast-math), so results are identical across the two builds. */
+#define O2_ARGS                                                                                   \
+    float *node, float *ctx, int d, const int32_t *walks, int64_t P, int L, const uint64_t *seeds, \
+        int window, int negative, const uint32_t *table, uint64_t table_len, float lr,           \
+        float alpha, int dot_mode, float *work
+#define O2_PASS \
+    node, ctx, d, walks, P, L, seeds, window, negative, table, table_len, lr, alpha, dot_mode, work
+#define O1_ARGS                                                                                   \
+    float *node, int d, const int32_t *edges, int64_t E, const uint64_t *seeds, int negative,    \
+        const uint32_t *table, uint64_t table_len, float lr, int dot_mode, float *work
+#define O1_PASS node, d, edges, E, seeds, negative, table, table_len, lr, dot_mode, work
+__attribute__((target("avx2,fma"))) static int64_t sgns_o2_fma(O2_ARGS) {
+    return sgns_o2_body(O2_PASS);
+}
+static int64_t sgns_o2_base(O2_ARGS) { return sgns_o2_body(O2_PASS); }
+__attribute__((target("avx2,fma"))) static int64_t sgns_o1_fma(O1_ARGS) {
+    return sgns_o1_body(O1_PASS);
+}
+static int64_t sgns_o1_base(O1_ARGS) { return sgns_o1_body(O1_PASS); }
+static int use_fma = -1;
+static int have_fma(void) {
+    if (use_fma < 0) {
+        __builtin_cpu_init();
+        use_fma = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+    }
+    return use_fma;
+}
+
+int64_t oracle_sgns_o2(float *node, float *ctx, int d, const int32_t *walks, int64_t P, int L,
+                       const uint64_t *seeds, int window, int negative, const uint32_t *table,
+                       uint64_t table_len, float lr, float alpha, int dot_mode) {
+    if (!exp_table_ready) oracle_exp_table(NULL);
+    float *work = (float *)malloc(sizeof(float) * (size_t)d);
+    int64_t pairs = (have_fma() ? sgns_o2_fma : sgns_o2_base)(O2_PASS);
+    free(work);
+    return pairs;
+}
+
+int64_t oracle_sgns_o1(float *node, int d, const int32_t *edges, int64_t E,
+                       const uint64_t *seeds, int negative, const uint32_t *table,
+                       uint64_t table_len, float lr, int dot_mode) {
+    if (!exp_table_ready) oracle_exp_table(NULL);
+    float *work = (float *)malloc(sizeof(float) * (size_t)d);
+    int64_t pairs = (have_fma() ? sgns_o1_fma : sgns_o1_base)(O1_PASS);
     free(work);
     return pairs;
 }

@@ -57,6 +57,7 @@ def lib():
         L.oracle_sgns_o1.restype = i64
         L.oracle_make_table.argtypes = [P, i64, P, u64, f64]
         L.oracle_min_margin.restype = f64
+        L.oracle_updates.restype = i64
         L.oracle_sgns_o2_hogwild.argtypes = [P, P, i64, i32, P, i64, i32, P, i32, i32, P, u64,
                                              f32, f32, i32, f64, P]
         L.oracle_sgns_o2_hogwild.restype = i64
@@ -92,6 +93,15 @@ def reset_margin():
 
 def min_margin():
     return float(lib().oracle_min_margin())
+
+
+def reset_updates():
+    lib().oracle_reset_updates()
+
+
+def updates():
+    """Target-row updates (targets past the +-6 skip) since reset_updates()."""
+    return int(lib().oracle_updates())
 
 
 def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha, dot_mode=DOT_REF):

@@ -41,8 +41,10 @@ def main(src, tag, kernel=KERNEL):
     alg = bench["roofline"]["bytes_per_pair"] * pairs
     m = re.search(r"d=(\d+), negative=(\d+)", cfg["workload"])
     dim, neg = int(m.group(1)), int(m.group(2))
+    ml = re.search(r"lr=([0-9.eE+-]+)", cfg["workload"])
     traffic = {"kernel": row["Name"], "tag": tag, "walks_per_launch": cfg["walks_per_step_per_gpu"],
-               "dim": dim, "negative": neg, "hbm_bytes_per_launch": read_b + write_b,
+               "dim": dim, "negative": neg, "lr": float(ml.group(1)) if ml else None,
+               "hbm_bytes_per_launch": read_b + write_b,
                "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
                "algorithmic_bytes_per_launch": alg, "pairs_per_launch": pairs,
                "rocprof_avg_kernel_ms": avg_ms,

@@ -57,3 +57,28 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libcome.so")
     with pytest.raises(_lib.ComeError, match="not found"):
         _lib.lib()
+
+
+def test_launch_options_snapshot_and_per_call_struct():
+    """come_set_option changes the process-wide snapshot that come_get_options returns; the
+    ctypes LaunchOpts mirrors come_launch_opts field for field; unknown names are rejected."""
+    L = _lib.lib()
+    o = _lib.launch_opts()
+    assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 1
+    assert o.o2_update_count is None
+    _lib.set_option("max_waves", 77)
+    try:
+        assert _lib.launch_opts().max_waves == 77
+        assert _lib.launch_opts(max_waves=5).max_waves == 5  # per call, process value unchanged
+        assert _lib.launch_opts().max_waves == 77
+    finally:
+        _lib.set_option("max_waves", 0)
+    with pytest.raises(_lib.ComeError, match="unknown option"):
+        _lib.set_option("no_such_knob", 1)
+    with pytest.raises(ValueError):
+        _lib.launch_opts(no_such_knob=1)
+    assert ctypes.sizeof(_lib.LaunchOpts) == 14 * 4 + 8  # 14 ints, then the pointer
+    p = ctypes.c_void_p(0)
+    rc = L.come_sgns_o2_ex(p, p, 0, 128, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p,
+                           ctypes.byref(o), p)
+    assert rc == -1 and b"V must be" in L.come_last_error()
