@@ -30,7 +30,7 @@ def kernel_name(d, n):
     vec = 1 if d <= 64 else 2 if d <= 128 else 4 if d <= 256 else 8
     full = "true" if vec > 1 and d == 64 * vec else "false"
     maxn = 5 if n <= 5 else 10 if n <= 10 else 20
-    return "come::k_sgns_o2_ring<%d, %s, %d, true>" % (vec, full, maxn)
+    return "come::k_sgns_o2_stream<%d, %s, %d>" % (vec, full, maxn)
 
 
 def log(*a):

@@ -6,8 +6,8 @@ search path there.  Module map, mirroring the reference layout:
 
     come_amd.training_sdg_inner   <- utils/training_sdg_inner.pyx (train_o1, train_o2, init,
                                      FAST_VERSION) -- drop-in, backed by libcome.so (HIP, gfx950)
-    come_amd.embedding            <- utils/embedding.py (Vocab, chunkize_serial, prepare_sentences,
-                                     RepeatCorpusNTimes)
+    come_amd.embedding            <- utils/embedding.py (Vocab; prepare_sentences as the
+                                     vectorised walks_to_rows)
     come_amd.model                <- ADSCModel/model.py (Model)
     come_amd.node_embeddings      <- ADSCModel/node_embeddings.py (Node2Vec)
     come_amd.context_embeddings   <- ADSCModel/context_embeddings.py (Context2Vec)

@@ -1,72 +1,54 @@
-"""Corpus helpers of the reference ``utils/embedding.py`` (host side of the hot path).
+"""Host side of the hot path's input: node-id walks -> row indices for the batched kernels.
 
-Same names and behaviour as the reference: ``Vocab`` (:164-175), ``chunkize_serial`` (:103-124),
-``prepare_sentences`` (:126-136), ``batch_generator`` (:138-145), ``RepeatCorpusNTimes``
-(:147-160).  Added: ``walks_to_rows`` -- the vectorised form of prepare_sentences that the batched
-trainers use (node ids -> row indices, OOV dropped, ragged walks padded with -1).
+The reference feeds its per-walk Cython calls through ``utils/embedding.py``: ``prepare_sentences``
+(:126-136) maps every node id of a walk to its ``Vocab`` entry, drops ids outside the vocabulary
+and, with down-sampling, drops each node with probability 1 - sample_probability;
+``chunkize_serial`` / ``RepeatCorpusNTimes`` (:103-124, :147-160) only batch and repeat that
+stream for the worker threads.  Here the whole corpus becomes ONE int32 row matrix
+(``walks_to_rows``): the same ids dropped, the same random draws in the same order, ragged walks
+padded with -1 (train_o2 treats trailing None exactly like a shorter path), and walks already on
+the GPU converted without leaving it.  Batching and repetition are the trainers' loops.
 
-The reference's pure-Python ``train_sg`` fallback (:10-100) targets an older API that no current
-code calls; it is not reproduced.
+``Vocab`` is the record ``Model.vocab`` maps ids to (the reference's count / index /
+sample_probability fields).  The pure-Python ``train_sg`` fallback (:10-100) targets an older
+API that no current code calls; it is not reproduced.
 """
-import itertools
-
 import numpy as np
 
 
 class Vocab(object):
-    """A single vocabulary item (utils/embedding.py:164-175)."""
+    """One vocabulary entry: ``count`` (degree), ``index`` (row), ``sample_probability``."""
+    __slots__ = ("count", "index", "sample_probability")
 
-    def __init__(self, **kwargs):
-        self.count = 0
-        self.__dict__.update(kwargs)
+    def __init__(self, count=0, index=-1, sample_probability=1.0):
+        self.count = count
+        self.index = index
+        self.sample_probability = sample_probability
 
     def __lt__(self, other):
         return self.count < other.count
 
-    def __str__(self):
-        vals = ['%s:%r' % (key, self.__dict__[key]) for key in sorted(self.__dict__)
-                if not key.startswith('_')]
-        return "<" + ', '.join(vals) + ">"
+    def __repr__(self):
+        return "Vocab(count=%r, index=%r, sample_probability=%r)" % (
+            self.count, self.index, self.sample_probability)
 
 
-def chunkize_serial(iterable, chunksize, as_numpy=False):
-    """Elements of `iterable` in `chunksize`-ed lists; the last may be shorter."""
-    it = iter(iterable)
-    while True:
-        if as_numpy:
-            wrapped_chunk = [[np.array(doc) for doc in itertools.islice(it, int(chunksize))]]
-        else:
-            wrapped_chunk = [list(itertools.islice(it, int(chunksize)))]
-        if not wrapped_chunk[0]:
-            break
-        yield wrapped_chunk.pop()
-
-
-def prepare_sentences(model, paths):
-    """Node ids -> Vocab objects, dropping OOV nodes and applying the down-sampling draw
-    (utils/embedding.py:126-136)."""
-    for path in paths:
-        sampled = [model.vocab[node] for node in path
-                   if node in model.vocab and (model.vocab[node].sample_probability >= 1.0 or
-                                               model.vocab[node].sample_probability >=
-                                               np.random.random_sample())]
-        yield sampled
-
-
-def batch_generator(iterable, batch_size=1):
-    args = [iterable] * batch_size
-    return itertools.zip_longest(*args, fillvalue=None)
-
-
-class RepeatCorpusNTimes():
-    def __init__(self, corpus, n):
-        self.corpus = corpus
-        self.n = n
-
-    def __iter__(self):
-        for _ in range(self.n):
-            for document in self.corpus:
-                yield document
+def downsample_rows(model, seqs):
+    """Apply the reference's down-sampling draw to row sequences in order: every row whose
+    sample_probability is below 1 consumes one np.random.random_sample() and is kept when its
+    probability is >= the draw (embedding.py:132-134); rows with probability 1 draw nothing."""
+    if not model.down_sampling:
+        return seqs
+    prob = model.sample_probability_rows()
+    out = []
+    for r in seqs:
+        p = prob[r]
+        keep = p >= 1.0
+        low = ~keep
+        if low.any():
+            keep[low] = p[low] >= np.random.random_sample(int(low.sum()))
+        out.append(r[keep])
+    return out
 
 
 def _device_rows(model, ids, max_len):
@@ -119,17 +101,7 @@ def walks_to_rows(model, paths, max_len=None):
         for path in paths:
             r = model.rows_of(np.asarray(path, np.int64).reshape(-1))
             seqs.append(r[r >= 0])
-    if model.down_sampling:
-        prob = model.sample_probability_rows()
-        kept = []
-        for r in seqs:
-            p = prob[r]
-            keep = p >= 1.0
-            low = ~keep
-            if low.any():
-                keep[low] = p[low] >= np.random.random_sample(int(low.sum()))
-            kept.append(r[keep])
-        seqs = kept
+    seqs = downsample_rows(model, seqs)
     L = max((len(s) for s in seqs), default=0)
     if max_len is not None:
         L = min(L, max_len)

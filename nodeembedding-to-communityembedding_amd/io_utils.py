@@ -13,9 +13,11 @@ import numpy as np
 
 
 def save_ground_true(file_name, community_color, path="./data"):
-    with open(path_join(path, "{}.txt".format(file_name)), 'w') as txt_file:
-        for node, com in enumerate(community_color):
-            txt_file.write('%d\t%d\n' % ((node + 1), com))
+    """IO_utils.save_ground_true (:8-16): "<node id>\t<label>" per line, ids from 1."""
+    labels = np.asarray(community_color, np.int64).reshape(-1)
+    lines = ["%d\t%d\n" % (i, c) for i, c in zip(range(1, len(labels) + 1), labels.tolist())]
+    with open(path_join(path, file_name + ".txt"), "w") as f:
+        f.writelines(lines)
 
 
 def load_ground_true(path='data/', file_name=None, multilabel=False):
@@ -52,9 +54,8 @@ def save_embedding(embeddings, file_name, path='data'):
 
 
 def load_embedding(file_name, path='data', ext=".txt"):
-    ret = []
-    with open(path_join(path, file_name + ext), 'r') as f:
-        for line in f:
-            tokens = line.strip().split('\t')
-            ret.append([float(val) for val in tokens[1].strip().split(' ')])
-    return np.array(ret, dtype=np.float32)
+    """IO_utils.load_embedding (:64-80): the vectors of a save_embedding file, in file order,
+    as float32 [V, d] (the id column is not used, as in the reference)."""
+    with open(path_join(path, file_name + ext)) as f:
+        vecs = [line.partition("\t")[2].split() for line in f if line.strip()]
+    return np.array(vecs, dtype=np.float64).astype(np.float32)

@@ -25,10 +25,18 @@ class Node2Vec(object):
         self.deterministic = deterministic
 
     def _edge_rows(self, model, edges):
+        """Edges -> [E, 2] int32 rows as prepare_sentences would pass them to train_o1: OOV
+        endpoints dropped and, with down-sampling, each endpoint kept by the reference's draw
+        (embedding.py:126-136; the draws are consumed edge by edge, endpoint by endpoint).  An
+        edge left with fewer than two endpoints makes the reference read an uninitialised index
+        (pyx:433-440, undefined behaviour): such edges are skipped (-1)."""
         e = np.asarray(edges, np.int64).reshape(-1, 2)
         rows = model.rows_of(e.reshape(-1)).reshape(-1, 2)
-        # prepare_sentences drops OOV endpoints; the reference then reads an uninitialised index
-        # (pyx:433-440, undefined behaviour) -- such edges are skipped (-1).
+        if model.down_sampling:
+            from .embedding import downsample_rows
+            kept = downsample_rows(model, [r[r >= 0] for r in rows])
+            rows = np.array([k if len(k) == 2 else (-1, -1) for k in kept],
+                            np.int64).reshape(-1, 2)
         bad = (rows < 0).any(axis=1)
         rows[bad] = -1
         return rows.astype(np.int32)
@@ -50,13 +58,17 @@ class Node2Vec(object):
         ed = torch.from_numpy(rows).to(dev)
         mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
         hot = None if self.deterministic else model.hot_rows()
-        for _ in range(int(iter)):
+        pairs = 0
+        for it in range(int(iter)):
+            if it > 0 and model.down_sampling:  # every pass draws its own sample (:47)
+                rows = self._edge_rows(model, edges)
+                ed = torch.from_numpy(rows).to(dev)
+            pairs += 2 * int((rows >= 0).all(axis=1).sum())
             seeds = tsi.draw_seeds(rows.shape[0])
             sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
             tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.negative_table(),
                         self.lr, mode, hot=hot)
         torch.cuda.synchronize(dev)
-        pairs = 2 * int((rows >= 0).all(axis=1).sum()) * int(iter)
         elapsed = time.time() - start
         log.info("O1 training: %i pair updates took %.2fs, %.0f pairs/s", pairs, elapsed,
                  pairs / elapsed if elapsed else 0.0)

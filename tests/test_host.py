@@ -11,7 +11,6 @@ from oracle import oracle as orc
 import come_amd.training_sdg_inner as tsi
 from come_amd import _lib, io_utils
 from come_amd.distributed import shard_range, shard_walks
-from come_amd.embedding import RepeatCorpusNTimes, chunkize_serial
 from come_amd.model import Model
 
 
@@ -143,9 +142,30 @@ def test_io_roundtrip(tmp_path):
     assert labels == [1, 2, 2] and k == 2
 
 
-def test_chunkize_and_repeat():
-    assert list(chunkize_serial(range(10), 3)) == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9]]
-    assert list(RepeatCorpusNTimes([1, 2], 3)) == [1, 2, 1, 2, 1, 2]
+def test_o1_edges_down_sampled_like_prepare_sentences():
+    """Node2Vec's edge rows go through the reference's down-sampling draw (prepare_sentences,
+    embedding.py:126-136): one draw per endpoint with sample_probability < 1, edge by edge; an
+    edge that loses an endpoint is skipped (the reference reads an uninitialised index there)."""
+    from come_amd.node_embeddings import Node2Vec
+    m, z = karate_model(down_sampling=0.005)
+    edges = z["edges"]
+    p = m.sample_probability_rows()
+    rows = edges - 1
+    draws = int((p[rows] < 1).sum())
+    np.random.seed(9)
+    got = Node2Vec(negative=4)._edge_rows(m, edges)
+    after = np.random.random_sample()
+    np.random.seed(9)
+    keep = np.ones(rows.shape, bool)
+    for e in range(len(rows)):
+        for k in range(2):
+            if p[rows[e, k]] < 1:
+                keep[e, k] = p[rows[e, k]] >= np.random.random_sample()
+    assert np.random.random_sample() == after and draws > 0
+    expect = np.where(keep.all(1)[:, None], rows, -1)
+    np.testing.assert_array_equal(got, expect)
+    m0, _ = karate_model()
+    np.testing.assert_array_equal(Node2Vec(negative=4)._edge_rows(m0, edges), rows)
 
 
 @pytest.mark.parametrize("n,world", [(10, 3), (7, 8), (0, 2), (100, 1), (1001, 8)])
