@@ -103,8 +103,10 @@ def _opts_arg(opts, update_count=None):
 
 
 # Rows holding at least this share of the negative table are "hot" (contended in Hogwild mode,
-# see come_hot.hip): measured on C3's shape (tests/test_gpu_tierc.py, scripts/diag_tierc.py).
-DEFAULT_HOT_P = 1e-5
+# see come_hot.hip).  Measured (scripts/diag_tierc.py, profiles/r02_ab_hot_threshold.txt): on
+# C3's shape at 100k nodes the held-out loss is 0.81% / 0.11% above the sequential oracle's at
+# shares 1e-5 / 5e-6; at C3 (1M nodes) 5e-6 marks 10k rows and costs no time vs 1e-5.
+DEFAULT_HOT_P = 5e-6
 
 
 def hot_rows(table, V, min_count):

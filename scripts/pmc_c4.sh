@@ -20,7 +20,8 @@ disp = collections.defaultdict(set)
 for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         kn = r.get("Kernel_Name", "")
-        for tag in ("k_community_mfma", "k_gmm_resp_mfma", "k_gmm_cov_mfma"):
+        for tag in ("k_community_async", "k_community_mfma", "k_gmm_resp_mfma", "k_gmm_cov_async",
+                    "k_gmm_cov_mfma"):
             if tag in kn:
                 key = (tag, r["Counter_Name"])
                 agg[key] += float(r["Counter_Value"])
