@@ -103,7 +103,8 @@ int come_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
 /* ---- Community gradient: replaces Community2Vec.train (community_embeddings.py:61-78) ----
  * x [V x d] updated in place, `iters` times:
  *   x_i -= lr * clip((beta/K) * sum_k pi[i,k] * inv_cov[k] @ (x_i - mu[k]), -5, 5)
- * pi [V x K], mu [K x d], inv_cov [K x d x d] (all device fp32).  d % 32 == 0 or d <= 32. */
+ * pi [V x K], mu [K x d], inv_cov [K x d x d] (all device fp32).  1 <= d <= 512 (MFMA kernels at
+ * d = 64, 128; VALU forms otherwise, the d x d matrices streamed in row chunks above d = 128). */
 int come_community_grad(float *x, int64_t V, int d, const float *pi, const float *mu,
                         const float *inv_cov, int K, float beta, float lr, int iters,
                         void *stream);
@@ -112,8 +113,9 @@ int come_community_grad(float *x, int64_t V, int d, const float *pi, const float
  * for covariance_type='full'.  prec_chol [K x d x d] (precision Cholesky factors, sklearn
  * layout), mu_prec [K x d] = mu_k @ prec_chol_k, log_norm [K] = log w_k + log det(prec_chol_k)
  * - d/2 log(2 pi) (all device fp32, precomputed on the host from the fitted parameters).
- * resp_out [V x K] device fp32.  K <= 64 (K <= 4096 for d = 64, 128: the MFMA path keeps the
- * per-component log-probabilities in resp_out itself). */
+ * resp_out [V x K] device fp32.  1 <= d <= 512.  K <= 64 for d <= 128 other than 64 and 128;
+ * K <= 4096 for d = 64, 128 and for d > 128 (those kernels keep the per-component
+ * log-probabilities in resp_out itself). */
 int come_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol, const float *mu_prec,
                   const float *log_norm, int K, float *resp_out, void *stream);
 
@@ -128,7 +130,7 @@ int come_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol, con
  * (x_i - means_k)^T (device fp32; covariance_k = scatter_k / nk_k + reg_covar I, sklearn
  * _estimate_gaussian_covariances_full).  Rows are split into `chunks` partial sums reduced in a
  * fixed order (deterministic); scratch: device fp32 [chunks x K x d x d] (unused when
- * chunks == 1).  d <= 128. */
+ * chunks == 1).  1 <= d <= 512. */
 int come_gmm_scatter(const float *x, int64_t V, int d, const float *resp, const float *means,
                      int K, int chunks, float *scratch, float *scatter_out, void *stream);
 
@@ -281,6 +283,12 @@ int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edges, int64_t
  * same clamp.  counts_by_id[0..V] (index 0 unused), table[T] (host memory).  O(V + T). */
 int come_make_table(const double *counts_by_id, int64_t V, uint32_t *table, uint64_t T,
                     double power);
+
+/* Host: the rows of `count` consecutive negative draws from next_random = seed (pyx:133-134:
+ * table[(nr >> 16) % T], then the LCG step), i.e. every row the walk's (edge's) negatives can
+ * touch: a train_o2 call on a walk with p pairs draws p * negative, train_o1 2 * negative. */
+int come_lcg_table_draws(uint64_t seed, int64_t count, const uint32_t *table, uint64_t T,
+                         uint32_t *out);
 
 /* Number of pair updates train_o2 performs on host walks [P x L] (-1 = None). */
 int64_t come_count_o2_pairs(const int32_t *walks, int64_t P, int L, int window);

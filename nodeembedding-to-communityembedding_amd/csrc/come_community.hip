@@ -846,6 +846,163 @@ __global__ void __launch_bounds__(256) k_gmm_cov_valu(CovArgs a) {
     }
 }
 
+// ---- wide rows (128 < d <= 512): VALU forms with the d x d matrices streamed in row chunks ----
+// The MFMA kernels above keep a whole d x d matrix (or a 128-row tile of inputs) in LDS, which
+// stops at d = 128.  These forms cover every d up to kMaxDim: kTRW rows per workgroup, each
+// component's matrix staged kChunkRows(d) rows at a time (<= 64 KiB, rows padded by one float
+// against bank conflicts).  Same arithmetic as k_community_grad / k_gmm_resp (fmaf chains in j
+// order), a fraction of the MFMA rate: they exist so that every embedding size the SGNS kernels
+// accept also trains through the community step (community_embeddings.py:61-78) and the GMM.
+constexpr int kTRW = 8;
+__host__ __device__ inline int chunk_rows(int d) { return 16384 / (d + 1); }
+
+__global__ void __launch_bounds__(kThreads) k_community_grad_wide(CommArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int d = a.d, CH = chunk_rows(d), LDM = d + 1;
+    float *X = smem;            // [kTRW][d]
+    float *Dk = X + kTRW * d;   // [kTRW][d]  x - mu_k
+    float *G = Dk + kTRW * d;   // [kTRW][d]
+    float *M = G + kTRW * d;    // [CH][d + 1] rows c0 .. c0 + CH of inv_cov[k]
+    float *P = M + CH * LDM;    // [kTRW] pi[:, k]
+    const int64_t r0 = (int64_t)blockIdx.x * kTRW;
+    const int rows = (int)((a.V - r0) < kTRW ? (a.V - r0) : kTRW);
+    const int n = kTRW * d;
+    for (int o = threadIdx.x; o < n; o += kThreads)
+        X[o] = o / d < rows ? a.x[(r0 + o / d) * d + (o % d)] : 0.0f;
+    for (int it = 0; it < a.iters; ++it) {
+        for (int o = threadIdx.x; o < n; o += kThreads) G[o] = 0.0f;
+        for (int k = 0; k < a.K; ++k) {
+            __syncthreads();
+            for (int o = threadIdx.x; o < n; o += kThreads) Dk[o] = X[o] - a.mu[k * d + (o % d)];
+            if (threadIdx.x < kTRW)
+                P[threadIdx.x] = threadIdx.x < rows ? a.pi[(r0 + threadIdx.x) * a.K + k] : 0.0f;
+            for (int c0 = 0; c0 < d; c0 += CH) {
+                const int cn = d - c0 < CH ? d - c0 : CH;
+                __syncthreads();
+                for (int o = threadIdx.x; o < cn * d; o += kThreads)
+                    M[(o / d) * LDM + o % d] = a.inv_cov[(int64_t)k * d * d + (int64_t)c0 * d + o];
+                __syncthreads();
+                for (int o = threadIdx.x; o < kTRW * cn; o += kThreads) {
+                    const int r = o / cn, c = o % cn;
+                    if (r >= rows) continue;
+                    float acc = 0.0f;
+                    for (int j = 0; j < d; ++j) acc = __builtin_fmaf(Dk[r * d + j], M[c * LDM + j], acc);
+                    G[r * d + c0 + c] = __builtin_fmaf(P[r], acc, G[r * d + c0 + c]);
+                }
+            }
+        }
+        __syncthreads();
+        for (int o = threadIdx.x; o < n; o += kThreads) {
+            float g = G[o] * a.coef;
+            g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);  // clip(min=-5, max=5), :79
+            X[o] = X[o] - g * a.lr;
+        }
+        __syncthreads();
+    }
+    for (int o = threadIdx.x; o < n; o += kThreads)
+        if (o / d < rows) a.x[(r0 + o / d) * d + (o % d)] = X[o];
+}
+
+// log N(x; mu_k, P_k) + log w_k for every (row, k) into resp_out (any K), then the per-row
+// softmax over k in place (the lse of each row optionally into a.lse).
+__global__ void __launch_bounds__(kThreads) k_gmm_resp_wide(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int d = a.d, CH = chunk_rows(d), LDM = d + 1;
+    float *X = smem;            // [kTRW][d]
+    float *Y = X + kTRW * d;    // [kTRW][d]  x P_k, accumulated over row chunks of P_k
+    float *M = Y + kTRW * d;    // [CH][d + 1] rows j0 .. j0 + CH of prec_chol[k]
+    float *SQ = M + CH * LDM;   // [kTRW]
+    const int64_t r0 = (int64_t)blockIdx.x * kTRW;
+    const int rows = (int)((a.V - r0) < kTRW ? (a.V - r0) : kTRW);
+    const int n = kTRW * d;
+    for (int o = threadIdx.x; o < n; o += kThreads)
+        X[o] = o / d < rows ? a.x[(r0 + o / d) * d + (o % d)] : 0.0f;
+    for (int k = 0; k < a.K; ++k) {
+        __syncthreads();
+        for (int o = threadIdx.x; o < n; o += kThreads) Y[o] = 0.0f;
+        if (threadIdx.x < kTRW) SQ[threadIdx.x] = 0.0f;
+        for (int j0 = 0; j0 < d; j0 += CH) {
+            const int jn = d - j0 < CH ? d - j0 : CH;
+            __syncthreads();
+            for (int o = threadIdx.x; o < jn * d; o += kThreads)
+                M[(o / d) * LDM + o % d] = a.prec_chol[(int64_t)k * d * d + (int64_t)j0 * d + o];
+            __syncthreads();
+            for (int o = threadIdx.x; o < n; o += kThreads) {
+                const int r = o / d, c = o % d;
+                float acc = Y[o];
+                for (int j = 0; j < jn; ++j)
+                    acc = __builtin_fmaf(X[r * d + j0 + j], M[j * LDM + c], acc);
+                Y[o] = acc;
+            }
+        }
+        __syncthreads();
+        for (int o = threadIdx.x; o < n; o += kThreads) {
+            const float y = Y[o] - a.mu_prec[k * d + (o % d)];
+            atomicAdd(&SQ[o / d], y * y);
+        }
+        __syncthreads();
+        if (threadIdx.x < rows) a.resp[(r0 + threadIdx.x) * a.K + k] =
+            a.log_norm[k] - 0.5f * SQ[threadIdx.x];
+    }
+    __syncthreads();
+    if (threadIdx.x < rows) {  // stores above came from this same thread: visible to it
+        float *lp = a.resp + (r0 + threadIdx.x) * a.K;
+        float m = -INFINITY;
+        for (int k = 0; k < a.K; ++k) m = fmaxf(m, lp[k]);
+        float s = 0.0f;
+        for (int k = 0; k < a.K; ++k) s += expf(lp[k] - m);
+        const float lse = m + logf(s);
+        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+        if (a.lse) a.lse[r0 + threadIdx.x] = lse;
+    }
+}
+
+// Scatter matrices for any d <= kMaxDim: workgroup (k, chunk, tile) accumulates the 64 x 64
+// output tile `tile` (row-major over (d/64 rounded up)^2 tiles) over the chunk's samples, staged
+// 32 at a time centred on mu_k with their weights.
+constexpr int kCovWideRB = 32;
+__global__ void __launch_bounds__(kThreads) k_gmm_cov_wide(CovArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int d = a.d, k = blockIdx.x, tid = threadIdx.x;
+    const int nt = (d + 63) / 64;
+    const int ti = blockIdx.z / nt, tj = blockIdx.z % nt;
+    float *xs = smem;                 // [kCovWideRB][d]
+    float *ws = xs + kCovWideRB * d;  // [kCovWideRB]
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    float acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    for (int64_t b = c0; b < c1; b += kCovWideRB) {
+        __syncthreads();
+        for (int o = tid; o < kCovWideRB * d; o += kThreads) {
+            const int s = o / d, c = o % d;
+            xs[o] = b + s < c1 ? a.x[(b + s) * d + c] - a.means[k * d + c] : 0.0f;
+        }
+        if (tid < kCovWideRB) ws[tid] = b + tid < c1 ? a.resp[(b + tid) * a.K + k] : 0.0f;
+        __syncthreads();
+        const int nb = (int)((c1 - b) < kCovWideRB ? (c1 - b) : kCovWideRB);
+        for (int s = 0; s < nb; ++s) {
+            const float w = ws[s];
+            const float *row = xs + s * d;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int e = tid + 256 * q;  // (i, j) of the 64 x 64 tile
+                const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
+                if (i < d && j < d) acc[q] = __builtin_fmaf(w * row[i], row[j], acc[q]);
+            }
+        }
+    }
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * d * d;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int e = tid + 256 * q;
+        const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
+        if (i < d && j < d) out[(int64_t)i * d + j] = acc[q];
+    }
+}
+
 // out[i] = sum_c part[c][i] in chunk order (deterministic), i over K d^2 entries.
 __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float *out, int64_t n,
                                                         int chunks) {
@@ -863,8 +1020,9 @@ using namespace come;
 extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, const float *mu,
                                    const float *inv_cov, int K, float beta, float lr, int iters,
                                    void *stream) {
-    if (V < 0 || d < 1 || d > 128 || K < 1 || iters < 0)
-        return set_error(COME_E_INVALID, "community_grad: need V>=0, 1<=d<=128, K>=1, iters>=0");
+    if (V < 0 || d < 1 || d > kMaxDim || K < 1 || iters < 0)
+        return set_error(COME_E_INVALID, "community_grad: need V>=0, 1<=d<=%d, K>=1, iters>=0",
+                         kMaxDim);
     if (V == 0 || iters == 0) return COME_OK;
     if (!x || !pi || !mu || !inv_cov) return set_error(COME_E_INVALID, "null pointer");
     int dev;
@@ -903,6 +1061,19 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
         return hip_error(hipGetLastError(), "k_community_mfma launch");
     }
+    if (d > 128) {
+        const size_t lds = sizeof(float) * ((size_t)3 * kTRW * d +
+                                            (size_t)chunk_rows(d) * (d + 1) + kTRW);
+        static bool attr_w = false;
+        if (!attr_w) {
+            (void)hipFuncSetAttribute((const void *)k_community_grad_wide,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_w = true;
+        }
+        hipLaunchKernelGGL(k_community_grad_wide, dim3((unsigned)((V + kTRW - 1) / kTRW)),
+                           dim3(kThreads), lds, (hipStream_t)stream, a);
+        return hip_error(hipGetLastError(), "k_community_grad_wide launch");
+    }
     const size_t lds = sizeof(float) * ((size_t)3 * kTR * d + (size_t)d * d);
     const unsigned grid = (unsigned)((V + kTR - 1) / kTR);
     static bool attr = false;
@@ -926,9 +1097,9 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
                               float *lse_out, void *stream) {
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)prec_chol % 16) == 0 &&
                       ((uintptr_t)mu_prec % 16) == 0;
-    if (V < 0 || d < 1 || d > 128 || K < 1 || K > 4096 || (!mfma && K > 64))
-        return set_error(COME_E_INVALID, "gmm_resp: need V>=0, 1<=d<=128, 1<=K<=64 (K<=4096 "
-                                         "for d = 64, 128)");
+    if (V < 0 || d < 1 || d > kMaxDim || K < 1 || K > 4096 || (!mfma && d <= 128 && K > 64))
+        return set_error(COME_E_INVALID, "gmm_resp: need V>=0, 1<=d<=%d, 1<=K<=4096 (K<=64 for "
+                                         "d <= 128 other than 64, 128)", kMaxDim);
     if (V == 0) return COME_OK;
     if (!x || !prec_chol || !mu_prec || !log_norm || !resp_out)
         return set_error(COME_E_INVALID, "null pointer");
@@ -958,6 +1129,19 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
         return hip_error(hipGetLastError(), "k_gmm_resp_mfma launch");
     }
+    if (d > 128) {
+        const size_t lds = sizeof(float) * ((size_t)2 * kTRW * d +
+                                            (size_t)chunk_rows(d) * (d + 1) + kTRW);
+        static bool attr_w = false;
+        if (!attr_w) {
+            (void)hipFuncSetAttribute((const void *)k_gmm_resp_wide,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_w = true;
+        }
+        hipLaunchKernelGGL(k_gmm_resp_wide, dim3((unsigned)((V + kTRW - 1) / kTRW)),
+                           dim3(kThreads), lds, (hipStream_t)stream, a);
+        return hip_error(hipGetLastError(), "k_gmm_resp_wide launch");
+    }
     const size_t lds = sizeof(float) * ((size_t)kTR * d + (size_t)d * d + kTR * 64 + kTR);
     const unsigned grid = (unsigned)((V + kTR - 1) / kTR);
     static bool attr = false;
@@ -973,9 +1157,9 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
 extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *resp,
                                 const float *means, int K, int chunks, float *scratch,
                                 float *scatter_out, void *stream) {
-    if (V < 0 || d < 1 || d > 128 || K < 1 || chunks < 1 || chunks > 65535)
-        return set_error(COME_E_INVALID, "gmm_scatter: need V>=0, 1<=d<=128, K>=1, "
-                                         "1<=chunks<=65535");
+    if (V < 0 || d < 1 || d > kMaxDim || K < 1 || chunks < 1 || chunks > 65535)
+        return set_error(COME_E_INVALID, "gmm_scatter: need V>=0, 1<=d<=%d, K>=1, "
+                                         "1<=chunks<=65535", kMaxDim);
     if (!x || !resp || !means || !scatter_out || (chunks > 1 && !scratch))
         return set_error(COME_E_INVALID, "null pointer");
     int dev;
@@ -988,6 +1172,23 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const int used = V == 0 ? 1 : (int)((V + per - 1) / per);
     CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K};
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
+    if (d > 128) {
+        const int nt = (d + 63) / 64;
+        const size_t lds = sizeof(float) * ((size_t)kCovWideRB * d + kCovWideRB);
+        static bool attr_w = false;
+        if (!attr_w) {
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_wide,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_w = true;
+        }
+        hipLaunchKernelGGL(k_gmm_cov_wide, dim3(K, used, nt * nt), dim3(kThreads), lds,
+                           (hipStream_t)stream, a);
+        rc = hip_error(hipGetLastError(), "k_gmm_cov_wide launch");
+        if (rc || used == 1) return rc;
+        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+    }
     const bool cov_async = current_opts().gmm_cov_async != 0;
     void (*kern)(CovArgs) =
         !mfma ? k_gmm_cov_valu

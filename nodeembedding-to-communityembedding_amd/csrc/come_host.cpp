@@ -249,3 +249,15 @@ extern "C" int64_t come_count_o2_pairs(const int32_t *walks, int64_t P, int L, i
     }
     return total;
 }
+
+extern "C" int come_lcg_table_draws(uint64_t seed, int64_t count, const uint32_t *table,
+                                    uint64_t T, uint32_t *out) {
+    if (count < 0 || (count > 0 && (!table || !out || T == 0)))
+        return set_error(COME_E_INVALID, "lcg_table_draws: bad arguments");
+    uint64_t nr = seed & kLcgMask;
+    for (int64_t i = 0; i < count; ++i) {  // pyx:133-134: draw, then advance
+        out[i] = table[(nr >> 16) % T];
+        nr = (nr * kLcgMul + kLcgAdd) & kLcgMask;
+    }
+    return COME_OK;
+}

@@ -296,9 +296,9 @@ class GaussianMixture(object):
         if self._n_total < self.n_components:
             raise ValueError("Expected n_samples >= n_components but got n_components = %d, "
                              "n_samples = %d" % (self.n_components, self._n_total))
-        if d > 128 or self.n_components > (4096 if d in (64, 128) else 64):
-            raise ValueError("GPU GaussianMixture supports d <= 128 and n_components <= 64 "
-                             "(<= 4096 for d = 64, 128)")
+        if d > 512 or self.n_components > (4096 if d in (64, 128) or d > 128 else 64):
+            raise ValueError("GPU GaussianMixture supports d <= 512 and n_components <= 64 "
+                             "(<= 4096 for d = 64, 128 and d > 128)")
         gen = self._generator(X.device)
         best, max_lb = None, -np.inf
         self.converged_ = False

@@ -188,69 +188,169 @@ def _rows_of(items):
     return np.array([-1 if it is None else int(it.index) for it in items], np.int32)
 
 
-class _DeviceTables:
-    """Resolve reference-style arguments (numpy or CUDA tensors) to CUDA tensors and write numpy
-    arguments back in place afterwards."""
+class _Mirrors(object):
+    """Device mirrors of the numpy arrays the per-call drop-ins are handed.
 
-    def __init__(self, *arrays):
+    The reference borrows its numpy buffers with no copy (pyx:410-411,457-459).  Copying whole
+    tables per call (400 MB for a 1e8-slot negative table, V x d per embedding table) would make
+    every call O(V + T), so:
+      * a numpy embedding table gets ONE device buffer of its shape, kept across calls (keyed by
+        the array's buffer address, shape and dtype) and never uploaded whole: each call uploads
+        exactly the rows it can touch and downloads the same rows afterwards (rows outside the
+        call are not read by the kernel, so their device contents do not matter);
+      * a numpy negative table is uploaded once and kept, keyed by buffer address and size and
+        re-checked per call against a fingerprint of 64 strided entries plus both ends (the
+        reference never mutates it after make_table, model.py:97-122; a table rewritten in place
+        with the same fingerprint is not detected -- pass a new array instead).
+    Per-call cost is O(rows a walk / edge can touch), independent of V and T."""
+
+    def __init__(self):
+        self.tables = {}
+        self.neg = {}
+
+    def table(self, arr, device):
         import torch
-        self.orig = arrays
-        self.dev = []
-        for a in arrays:
-            if isinstance(a, torch.Tensor):
-                if not a.is_cuda:
-                    raise TypeError("tables must be CUDA tensors or numpy arrays")
-                self.dev.append(a)
-            else:
-                self.dev.append(torch.from_numpy(np.ascontiguousarray(a)).cuda())
+        key = (arr.__array_interface__["data"][0], arr.shape, arr.dtype.str, str(device))
+        t = self.tables.get(key)
+        if t is None:
+            if len(self.tables) >= 16:  # bounded: a long-running caller cycling arrays
+                self.tables.clear()
+            t = self.tables[key] = torch.empty(arr.shape, dtype=torch.float32, device=device)
+        return t
 
-    def writeback(self, *which):
+    @staticmethod
+    def _fingerprint(arr):
+        idx = np.linspace(0, len(arr) - 1, 64).astype(np.int64)
+        return arr[idx].tobytes()
+
+    def negative_table(self, arr, device):
         import torch
-        for i in which:
-            if not isinstance(self.orig[i], torch.Tensor):
-                np.copyto(self.orig[i], self.dev[i].cpu().numpy())
+        arr = np.ascontiguousarray(arr, np.uint32)
+        key = (arr.__array_interface__["data"][0], arr.shape[0], str(device))
+        fp = self._fingerprint(arr)
+        hit = self.neg.get(key)
+        if hit is None or hit[0] != fp:
+            if len(self.neg) >= 4:
+                self.neg.clear()
+            hit = self.neg[key] = (fp, torch.from_numpy(arr.view(np.int32)).to(device))
+        return hit[1]
 
 
-def _table_tensor(py_table):
+_MIRRORS = _Mirrors()
+
+
+def _device_of(*arrays):
+    import torch
+    for a in arrays:
+        if isinstance(a, torch.Tensor):
+            if not a.is_cuda:
+                raise TypeError("tables must be CUDA tensors or numpy arrays")
+            return a.device
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _resolve_table(py_table, device):
+    """The negative table as a CUDA int32 tensor and as host uint32 numpy (None when it is a
+    tensor: then the touched rows are not computed on the host)."""
     import torch
     if isinstance(py_table, torch.Tensor):
-        return py_table if py_table.dtype == torch.int32 else py_table.view(torch.int32)
-    return torch.from_numpy(np.ascontiguousarray(py_table, np.uint32).view(np.int32)).cuda()
+        t = py_table if py_table.dtype == torch.int32 else py_table.view(torch.int32)
+        return t.to(device), None
+    host = np.ascontiguousarray(py_table, np.uint32)
+    return _MIRRORS.negative_table(host, device), host
+
+
+def _draw_rows(seed, count, host_table):
+    """Rows of `count` consecutive negative draws from `seed` (come_lcg_table_draws)."""
+    out = np.empty(int(count), np.uint32)
+    if count:
+        check(_lib.lib().come_lcg_table_draws(int(seed), int(count), ptr(host_table),
+                                              host_table.shape[0], ptr(out)),
+              "come_lcg_table_draws")
+    return out.astype(np.int64)
+
+
+class _Borrowed(object):
+    """One reference-style table argument for one call: a CUDA tensor is used as is; a numpy
+    array goes through its device mirror, `rows` up before the launch and down after it."""
+
+    def __init__(self, arr, device, rows):
+        import torch
+        self.arr = arr
+        if isinstance(arr, torch.Tensor):
+            self.dev, self.rows = arr, None
+            return
+        if not (isinstance(arr, np.ndarray) and arr.dtype == np.float32 and arr.ndim == 2 and
+                arr.flags.c_contiguous):
+            raise TypeError("embedding tables must be C-contiguous float32 [V, d] numpy arrays "
+                            "or CUDA tensors")
+        self.dev = _MIRRORS.table(arr, device)
+        r = np.unique(rows)
+        self.rows = r[(r >= 0) & (r < arr.shape[0])]
+        if len(self.rows):
+            ri = torch.from_numpy(self.rows).to(device)
+            self.ridx = ri
+            self.dev.index_copy_(0, ri, torch.from_numpy(arr[self.rows]).to(device))
+
+    def writeback(self):
+        if self.rows is not None and len(self.rows):
+            self.arr[self.rows] = self.dev.index_select(0, self.ridx).cpu().numpy()
 
 
 def train_o2(py_node_embedding, py_context_embedding, py_path, py_lr, py_negative, py_window,
              py_table, py_alpha=1.0, py_size=None, py_work=None):
-    """One walk (pyx:454-509).  Returns the number of non-None entries."""
+    """One walk (pyx:454-509).  Returns the number of non-None entries.  Tables may be CUDA
+    tensors (used in place) or numpy arrays (mutated in place through cached device mirrors,
+    moving only the rows this walk can touch; see _Mirrors)."""
     import torch
     nr = int(draw_seeds(1)[0])  # pyx:477: two draws from the global numpy RNG, per call
     items = list(py_path)[:MAX_SENTENCE_LEN]
     rows = _rows_of(items)
     result = int((rows >= 0).sum())
-    t = _DeviceTables(py_node_embedding, py_context_embedding)
-    dev = t.dev[0].device
-    walks = torch.from_numpy(rows.reshape(1, -1)).to(dev)
-    seeds = torch.tensor([nr], dtype=torch.int64).view(1).to(dev) if nr < 2 ** 63 else \
-        torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(dev)
-    if rows.size:
-        sgns_o2(t.dev[0], t.dev[1], walks, seeds, py_window, py_negative,
-                _table_tensor(py_table).to(dev), py_lr, py_alpha, MODE_SEQUENTIAL)
-    t.writeback(0, 1)
+    if not rows.size:
+        return result
+    device = _device_of(py_node_embedding, py_context_embedding, py_table)
+    table, host_table = _resolve_table(py_table, device)
+    walk_rows = rows[rows >= 0].astype(np.int64)
+    ctx_rows = walk_rows
+    numpy_ctx = not isinstance(py_context_embedding, torch.Tensor)
+    if numpy_ctx:  # positives are walk rows; negatives come from this call's draws
+        if host_table is None:
+            host_table = table.cpu().numpy().view(np.uint32)
+        pairs = count_o2_pairs(rows.reshape(1, -1), py_window)
+        ctx_rows = np.concatenate([walk_rows, _draw_rows(nr, pairs * int(py_negative),
+                                                         host_table)])
+    node = _Borrowed(py_node_embedding, device, walk_rows)
+    ctx = _Borrowed(py_context_embedding, device, ctx_rows)
+    walks = torch.from_numpy(rows.reshape(1, -1)).to(device)
+    seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(device)
+    sgns_o2(node.dev, ctx.dev, walks, seeds, py_window, py_negative, table, py_lr, py_alpha,
+            MODE_SEQUENTIAL)
+    node.writeback()
+    ctx.writeback()
     return result
 
 
 def train_o1(py_node_embedding, py_edge, py_lr, py_negative, py_table, py_size=None, py_work=None):
     """One edge (pyx:407-450): pairs (edge[0] -> edge[1]) then (edge[1] -> edge[0]).  Returns the
-    number of non-None endpoints."""
+    number of non-None endpoints.  numpy tables: only the edge's rows and its 2n negative rows
+    cross to and from the device."""
     import torch
     nr = int(draw_seeds(1)[0])  # pyx:427
     rows = _rows_of(list(py_edge)[:2])
     result = int((rows >= 0).sum())
-    t = _DeviceTables(py_node_embedding)
-    dev = t.dev[0].device
-    if rows.size == 2:
-        edges = torch.from_numpy(rows.reshape(1, 2)).to(dev)
-        seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(dev)
-        sgns_o1(t.dev[0], edges, seeds, py_negative, _table_tensor(py_table).to(dev), py_lr,
-                MODE_SEQUENTIAL)
-    t.writeback(0)
+    if rows.size != 2:
+        return result
+    device = _device_of(py_node_embedding, py_table)
+    table, host_table = _resolve_table(py_table, device)
+    touched = rows[rows >= 0].astype(np.int64)
+    if not isinstance(py_node_embedding, torch.Tensor):
+        if host_table is None:
+            host_table = table.cpu().numpy().view(np.uint32)
+        touched = np.concatenate([touched, _draw_rows(nr, 2 * int(py_negative), host_table)])
+    node = _Borrowed(py_node_embedding, device, touched)
+    edges = torch.from_numpy(rows.reshape(1, 2)).to(device)
+    seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(device)
+    sgns_o1(node.dev, edges, seeds, py_negative, table, py_lr, MODE_SEQUENTIAL)
+    node.writeback()
     return result

@@ -41,7 +41,8 @@ def problem(V, K, d, seed, sep=3.0):
     return X.astype(np.float32), w, mu, cov
 
 
-@pytest.mark.parametrize("V,K,d", [(1000, 4, 8), (3000, 6, 64), (2500, 5, 128), (777, 3, 100)])
+@pytest.mark.parametrize("V,K,d", [(1000, 4, 8), (3000, 6, 64), (2500, 5, 128), (777, 3, 100),
+                                   (900, 4, 256), (300, 70, 200)])
 def test_estep_vs_numpy(V, K, d):
     X, w, mu, cov = problem(V, K, d, V + d)
     pc = orc.precision_cholesky(cov)
@@ -89,7 +90,8 @@ def test_estep_mixed_factor_shapes(d):
 
 
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
-                                          (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None)])
+                                          (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None),
+                                          (1500, 3, 256, 4), (200, 2, 330, None)])
 def test_scatter_vs_numpy(V, K, d, chunks):
     rng = np.random.RandomState(V + K)
     X = rng.normal(size=(V, d)).astype(np.float32)
@@ -202,3 +204,28 @@ def test_scatter_async_matches_sync(V, K, d, chunks):
     finally:
         _lib.set_option("gmm_cov_async", 1)
     np.testing.assert_array_equal(out[0], out[1])
+
+
+def test_community2vec_trains_at_d256():
+    """A model with layer1_size = 256 (the SGNS kernels' C5 width) goes through the whole
+    community phase: GPU GMM fit, responsibilities, community step (wide VALU kernels); the
+    sklearn backend too (its predict_proba goes through come_gmm_resp as well)."""
+    from come_amd.community_embeddings import Community2Vec
+    from come_amd.model import Model
+    V, d, K = 1200, 256, 3
+    X, w, mu, cov = problem(V, K, d, 5, sep=4.0)
+    for backend in ("gpu", "sklearn"):
+        np.random.seed(0)
+        m = Model((np.arange(1, V + 1), np.full(V, 3)), size=d, table_size=10000, k=K,
+                  device=dev())
+        m.node_embedding = torch.as_tensor(X, device=dev())
+        cm = Community2Vec(m, lr=0.1, reg_covar=1e-5, gmm_backend=backend)
+        cm.g_mixture.n_init = 1
+        cm.fit(m)
+        pi = m.pi.cpu().numpy()
+        assert pi.shape == (V, K) and np.allclose(pi.sum(1), 1, atol=1e-4)
+        x0 = m.node_embedding.clone()
+        cm.train(range(1, V + 1), m, 0.1, iter=2)
+        ref = orc.community_train(x0.cpu().numpy(), pi, m.centroid.cpu().numpy(),
+                                  m.inv_covariance_mat.cpu().numpy(), 0.1, 0.1, 2)
+        np.testing.assert_allclose(m.node_embedding.cpu().numpy(), ref, rtol=2e-5, atol=2e-5)

@@ -244,6 +244,46 @@ def test_o2_dropin_per_walk_numpy_and_tensor():
     np.testing.assert_array_equal(tnode.cpu().numpy(), node)
 
 
+def test_dropin_per_call_cost_independent_of_table_sizes():
+    """The per-call drop-ins move only the rows a walk / edge can touch (numpy tables through
+    cached device mirrors, the negative table uploaded once): per-call time must not grow with
+    T (1e4 -> 2e7 slots) or V (2e3 -> 2e6 rows), and the numpy results must equal the CUDA-tensor
+    path's bit for bit."""
+    import time
+
+    class V_:
+        def __init__(self, i):
+            self.index = i
+    rng = np.random.RandomState(12)
+    d, neg, w, calls = 64, 5, 3, 40
+    times = {}
+    for V, T in ((2000, 10_000), (2_000_000, 20_000_000)):
+        table = orc.make_table(rng.randint(1, 50, V), T)
+        node = rng.uniform(-1, 1, (V, d)).astype(np.float32)
+        ctx = np.zeros_like(node)
+        tnode, tctx, ttab = dev(node), dev(ctx), dev(table)
+        paths = [[V_(int(x)) for x in rng.randint(0, V, 30)] for _ in range(calls + 1)]
+        edges = [[V_(int(x)) for x in rng.randint(0, V, 2)] for _ in range(calls + 1)]
+        np.random.seed(3)
+        tsi.train_o2(node, ctx, paths[0], 0.05, neg, w, table)  # warm-up: uploads the table
+        tsi.train_o1(node, edges[0], 0.05, neg, table)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for p, e in zip(paths[1:], edges[1:]):
+            tsi.train_o2(node, ctx, p, 0.05, neg, w, table)
+            tsi.train_o1(node, e, 0.05, neg, table)
+        times[(V, T)] = (time.time() - t0) / calls
+        np.random.seed(3)
+        for p, e in zip(paths, edges):
+            tsi.train_o2(tnode, tctx, p, 0.05, neg, w, ttab)
+            tsi.train_o1(tnode, e, 0.05, neg, ttab)
+        np.testing.assert_array_equal(tnode.cpu().numpy(), node)
+        np.testing.assert_array_equal(tctx.cpu().numpy(), ctx)
+    small, big = times[(2000, 10_000)], times[(2_000_000, 20_000_000)]
+    print("per call: small tables %.3f ms, large tables %.3f ms" % (small * 1e3, big * 1e3))
+    assert big < 2.0 * small + 2e-3, times
+
+
 # ---- O1 ----------------------------------------------------------------------------------------
 
 @pytest.mark.parametrize("name", list(KAT_O1["names"]))
@@ -306,9 +346,10 @@ def test_community_grad_vs_golden():
 
 
 @pytest.mark.parametrize("d,V,K,iters", [(64, 1000, 7, 3), (128, 777, 5, 2), (128, 300, 1, 1),
-                                          (96, 200, 3, 2)])
+                                          (96, 200, 3, 2), (256, 150, 3, 2), (500, 37, 2, 1)])
 def test_community_grad_vs_oracle(d, V, K, iters):
-    """MFMA path (d = 64, 128; ragged row tiles) and VALU path (d = 96) against the numpy
+    """MFMA path (d = 64, 128; ragged row tiles), VALU path (d = 96) and the wide VALU path
+    (d = 256, 500: matrices streamed in row chunks) against the numpy
     restatement of community_embeddings.py:61-78: fp32 contractions in another order,
     rtol/atol 2e-5; the clip at +-5 is exercised (beta large)."""
     rng = np.random.RandomState(d + V)
