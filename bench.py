@@ -71,6 +71,52 @@ def calibration_ratio():
         return None, None
 
 
+def measure_sparse_sync(model, step, s, dev):
+    """One more training step from a snapshot, then the row-sparse exchange's local passes on
+    this GPU (come_delta_flags over both tables, the row compaction, come_delta_gather and
+    come_delta_scatter): rows changed per table and bytes an all-reduce would move per sync,
+    sparse vs dense, with HIP-event times of the passes.  The all-reduce itself
+    needs N > 1 (RCCL over xGMI)."""
+    import torch
+    from come_amd import _lib
+    from come_amd._lib import check, ptr, stream_handle
+    tabs = [model.node_embedding, model.context_embedding]
+    snaps = [t.clone() for t in tabs]
+    step(s)
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    st = stream_handle(dev)
+    ev[0].record()
+    flags = []
+    for t, sn in zip(tabs, snaps):
+        f = torch.empty(t.shape[0], dtype=torch.uint8, device=dev)
+        check(_lib.lib().come_delta_flags(ptr(t), ptr(sn), t.shape[0], t.shape[1], ptr(f), st),
+              "come_delta_flags")
+        flags.append(f)
+    ev[1].record()
+    idx = [torch.nonzero(f).view(-1) for f in flags]
+    bufs = [(t.new_empty((i.numel(), t.shape[1])), t.new_empty((i.numel(), t.shape[1])))
+            for t, i in zip(tabs, idx)]
+    torch.cuda.synchronize(dev)
+    ev[2].record()
+    for t, sn, i, (ds, do) in zip(tabs, snaps, idx, bufs):
+        check(_lib.lib().come_delta_gather(ptr(t), ptr(sn), ptr(i), i.numel(), t.shape[1],
+                                           ptr(ds), ptr(do), st), "come_delta_gather")
+        check(_lib.lib().come_delta_scatter(ptr(t), ptr(sn), ptr(i), i.numel(), t.shape[1],
+                                            ptr(ds), ptr(do), st), "come_delta_scatter")
+    ev[3].record()
+    torch.cuda.synchronize(dev)
+    rows = [int(i.numel()) for i in idx]
+    d = tabs[0].shape[1]
+    dense = sum(t.numel() * 4 for t in tabs)
+    sparse = sum(r * d * 4 for r in rows)
+    return {"rows_changed": {"node": rows[0], "context": rows[1]}, "rows_total": tabs[0].shape[0],
+            "bytes_per_sync_sparse": sparse, "bytes_per_sync_dense": dense,
+            "flags_ms": ev[0].elapsed_time(ev[1]), "gather_scatter_ms": ev[2].elapsed_time(ev[3]),
+            "note": "one step's changes; all-reduce payload per rank; replicas per rank: dense "
+                    "3 full copies (sync base + 2 exchange buffers), sparse 1 + [rows x d]"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -90,6 +136,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this process may use (affinity and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sparse-sync", action="store_true",
+                    help="N>1: exchange only the rows some rank changed (SparseDeltaAllReduce)")
+    ap.add_argument("--measure-sync", action="store_true",
+                    help="N=1: after the timed steps, measure the row-sparse exchange's local "
+                         "passes for one step (rows changed, bytes per sync, pass times)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: blocking delta all-reduce instead of overlapping it with the next "
                          "batch")
@@ -111,7 +162,7 @@ def main():
     import torch.distributed as dist
 
     import come_amd.training_sdg_inner as tsi
-    from come_amd.distributed import DeltaAllReduce
+    from come_amd.distributed import DeltaAllReduce, SparseDeltaAllReduce
     from come_amd.graph import chung_lu, random_walks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,7 +200,8 @@ def main():
     lengths = (walks_all >= 0).sum(dim=1)
     pairs_per_step = [int(o2_pairs_of_lengths(lengths[s * B:(s + 1) * B], w))
                       for s in range(total_steps)]
-    sync = DeltaAllReduce([model.node_embedding, model.context_embedding]) if world > 1 else None
+    sync_cls = SparseDeltaAllReduce if args.sparse_sync else DeltaAllReduce
+    sync = sync_cls([model.node_embedding, model.context_embedding]) if world > 1 else None
     # the reference's uint32 table, or its exact packed form (come_pack_table) with
     # --packed-table (same draws; 1% slower at C3 on MI355X, profiles/r01_ab_dynamic_sched.txt)
     neg_table = model.table_packed if args.packed_table and model.table_packed is not None \
@@ -272,6 +324,10 @@ def main():
                              "AVX2+FMA" if isa else "baseline-ISA", threads, cw, cp, cel,
                              rthreads, "%.3f" % ratio if ratio else "n/a")}
 
+    sync_measure = None
+    if world == 1 and args.measure_sync:
+        sync_measure = measure_sparse_sync(model, step, args.warmup, dev)
+
     value = total_pairs / elapsed
     out = {
         "metric": "SGNS pair-updates/sec at d=%d, %s-node graph" % (
@@ -320,6 +376,8 @@ def main():
         },
         "cpu_baseline": cpu,
     }
+    if sync_measure is not None:
+        out["sync_measure"] = sync_measure
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -204,6 +204,20 @@ int come_delta_begin(const float *W, const float *S, float *D, float *Down, int6
 int come_delta_end(float *W, float *S, const float *Dsum, const float *Down, int64_t n,
                    void *stream);
 
+/* Row-sparse exchange (come_amd.distributed.SparseDeltaAllReduce): only rows some rank changed.
+ * W, S: device fp32 [rows x d], d % 4 == 0, 16-byte aligned.
+ *   come_delta_flags:   flags[r] = 1 iff row r of W differs bitwise from S, else 0 (uint8 [rows])
+ *   come_delta_gather:  D[i] = W[idx[i]] - S[idx[i]]; Down = D    (D, Down: [n x d])
+ *   come_delta_scatter: S[idx[i]] += Dsum[i]; W[idx[i]] += Dsum[i] - Down[i]
+ * idx: device int64 [n] row indices.  A row no rank changed contributes exactly +0 to the dense
+ * exchange, so the sparse one leaves the tables bit-identical to it. */
+int come_delta_flags(const float *W, const float *S, int64_t rows, int d, uint8_t *flags,
+                     void *stream);
+int come_delta_gather(const float *W, const float *S, const int64_t *idx, int64_t n, int d,
+                      float *D, float *Down, void *stream);
+int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
+                       const float *Dsum, const float *Down, void *stream);
+
 /* ---- Launch options ----
  * Kernel-selection and grid knobs (0 = automatic unless stated):
  *   o2_kernel           1 = direct kernel, 2 = LDS-ring kernel (automatic: ring when it fits)

@@ -122,10 +122,19 @@ class Community2Vec(object):
         return all_gather_rows(pi, self.group)
 
     def train(self, nodes, model, beta, chunksize=150, iter=1):
+        """community_embeddings.py:61-78.  The reference walks `nodes` in chunks of `chunksize`
+        and adds each chunk's gradient with grad_input[node_index] += batch (numpy fancy-index
+        add: a node listed twice in ONE chunk counts once, a node in m different chunks m
+        times), then updates every row.  So row r moves by clip(m_r * coef * G_r) with m_r the
+        number of chunks that list it; here m_r scales pi's row (G is linear in it).  Ids outside
+        the vocabulary raise KeyError, as model.vocab[x] does."""
         import torch
-        rows = model.rows_of(np.fromiter((int(n) for n in nodes), np.int64))
-        rows = rows[rows >= 0]
+        ids = np.fromiter((int(n) for n in nodes), np.int64)
+        rows = model.rows_of(ids)
+        if (rows < 0).any():
+            raise KeyError(int(ids[np.argmax(rows < 0)]))
         x = model.node_embedding
+        chunksize = max(1, int(chunksize))
         if len(rows) == model.vocab_size and (np.sort(rows) == np.arange(len(rows))).all():
             lo, hi = self._shard(x.shape[0])
             if hi > lo:  # a row block of a C-contiguous table is itself contiguous
@@ -134,14 +143,20 @@ class Community2Vec(object):
             if self.distributed:
                 all_gather_rows(x, self.group)
             return
-        uniq = np.unique(rows)
+        # multiplicity: the number of chunks that list the row
+        chunk = np.arange(len(rows)) // chunksize
+        pairs = np.unique(chunk * np.int64(model.vocab_size) + rows)
+        uniq, mult = np.unique(pairs % model.vocab_size, return_counts=True)
         idx = torch.from_numpy(uniq).to(x.device)
         sub = x.index_select(0, idx).contiguous()
+        pi = model.pi.index_select(0, idx)
+        if (mult > 1).any():
+            pi = pi * torch.from_numpy(mult.astype(np.float32)).to(x.device)[:, None]
+        pi = pi.contiguous()
         lo, hi = self._shard(len(uniq))
         if hi > lo:
-            part = sub[lo:hi]
-            community_grad(part, model.pi.index_select(0, idx[lo:hi]).contiguous(),
-                           model.centroid, model.inv_covariance_mat, beta, self.lr, iter)
+            community_grad(sub[lo:hi], pi[lo:hi], model.centroid, model.inv_covariance_mat, beta,
+                           self.lr, iter)
         if self.distributed:
             all_gather_rows(sub, self.group)
         x.index_copy_(0, idx, sub)

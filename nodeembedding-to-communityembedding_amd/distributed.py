@@ -27,6 +27,13 @@ rank trained meanwhile:
 after which W - W_sync is exactly the rank's progress since ``start`` -- no update is lost or
 counted twice, and the replicas differ only by what each trained after ``start`` (Hogwild-style
 staleness of one batch).  ``sync`` = ``start`` + ``finish`` (no overlap).
+
+``SparseDeltaAllReduce`` is the same protocol over the rows some rank changed only: each rank
+flags the rows where W differs bitwise from W_sync, the flags are OR-ed across ranks (one uint8
+all-reduce MAX of V bytes), and only the union's rows are gathered, all-reduced and scattered
+back.  Unchanged rows have a delta of exactly +0 on every rank, so the tables end bit-identical
+to the dense exchange.  It keeps one full replica per table (W_sync) instead of three; the
+exchange buffers are [rows changed x d].
 """
 import numpy as np
 
@@ -176,6 +183,108 @@ class DeltaAllReduce(object):
 
     def bytes_per_sync(self):
         return sum(t.numel() * t.element_size() for t in self.tables)
+
+
+class SparseDeltaAllReduce(object):
+    """DeltaAllReduce restricted to the rows that changed on some rank (see the module docstring).
+    Same start / finish / sync protocol; ``last_rows`` / ``last_bytes`` report the previous
+    exchange (rows in the union, bytes all-reduced per rank)."""
+
+    def __init__(self, tables, group=None, bucket_elems=1 << 26):
+        import torch.distributed as dist
+        self.tables = list(tables)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.bucket = int(bucket_elems)
+        self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
+        self.pending = []
+        self.state = []
+        self.last_rows = [0] * len(self.tables)
+        self.last_bytes = 0
+
+    @staticmethod
+    def _flags(t, s):
+        import torch
+        if _fused(t) and t.shape[1] % 4 == 0:
+            from . import _lib
+            from ._lib import check, ptr, stream_handle
+            f = torch.empty(t.shape[0], dtype=torch.uint8, device=t.device)
+            check(_lib.lib().come_delta_flags(ptr(t), ptr(s), t.shape[0], t.shape[1], ptr(f),
+                                              stream_handle(t.device)), "come_delta_flags")
+            return f
+        return (t.view(torch.int32) != s.view(torch.int32)).any(dim=1).to(torch.uint8)
+
+    def start(self):
+        if self.world == 1:
+            return
+        import torch
+        import torch.distributed as dist
+        self.finish()
+        flags = [self._flags(t, s) for t, s in zip(self.tables, self.snap)]
+        flat = torch.cat(flags)
+        dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group)  # union over ranks
+        self.state = []
+        self.last_bytes = 0
+        o = 0
+        for i, (t, s) in enumerate(zip(self.tables, self.snap)):
+            idx = torch.nonzero(flat[o:o + t.shape[0]]).view(-1)
+            o += t.shape[0]
+            n, d = idx.numel(), t.shape[1]
+            ds = t.new_empty((n, d))
+            do = t.new_empty((n, d))
+            if n and _fused(t) and d % 4 == 0:
+                from . import _lib
+                from ._lib import check, ptr, stream_handle
+                check(_lib.lib().come_delta_gather(ptr(t), ptr(s), ptr(idx), n, d, ptr(ds),
+                                                   ptr(do), stream_handle(t.device)),
+                      "come_delta_gather")
+            elif n:
+                torch.sub(t.index_select(0, idx), s.index_select(0, idx), out=ds)
+                do.copy_(ds)
+            fl = ds.view(-1)
+            for lo in range(0, fl.numel(), self.bucket):
+                hi = min(lo + self.bucket, fl.numel())
+                self.pending.append(dist.all_reduce(fl[lo:hi], op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True))
+            self.state.append((idx, ds, do))
+            self.last_rows[i] = n
+            self.last_bytes += n * d * t.element_size()
+
+    def finish(self):
+        if self.world == 1 or not self.state:
+            return
+        for w in self.pending:
+            w.wait()
+        self.pending = []
+        for t, s, (idx, ds, do) in zip(self.tables, self.snap, self.state):
+            n, d = idx.numel(), t.shape[1]
+            if not n:
+                continue
+            if _fused(t) and d % 4 == 0:
+                from . import _lib
+                from ._lib import check, ptr, stream_handle
+                check(_lib.lib().come_delta_scatter(ptr(t), ptr(s), ptr(idx), n, d, ptr(ds),
+                                                    ptr(do), stream_handle(t.device)),
+                      "come_delta_scatter")
+            else:
+                s.index_add_(0, idx, ds)          # W_sync += sum_r D_r
+                t.index_add_(0, idx, ds - do)     # W += sum_r D_r - D_own
+        self.state = []
+
+    def sync(self):
+        """Blocking exchange; every replica then equals W_sync bit for bit (as DeltaAllReduce)."""
+        if self.world == 1:
+            return
+        self.start()
+        touched = [idx for idx, _, _ in self.state]
+        self.finish()
+        for t, s, idx in zip(self.tables, self.snap, touched):
+            if idx.numel():
+                t.index_copy_(0, idx, s.index_select(0, idx))
+
+    @property
+    def busy(self):
+        return bool(self.pending)
 
 
 def reference_delta_sum(w_sync, locals_):

@@ -216,9 +216,9 @@ class GaussianMixture(object):
             s2 = (X.double() ** 2).sum(0)
             all_reduce_sum([s1, s2], self.group)
             n = float(self._n_total)
-            tol = self.kmeans_tol * float(((s2 - s1 * s1 / n) / (n - 1)).mean())
+            tol = self.kmeans_tol * float(((s2 - s1 * s1 / n) / n).mean())  # np.var: ddof 0
         else:
-            tol = self.kmeans_tol * float(X.var(0).mean())
+            tol = self.kmeans_tol * float(X.var(0, unbiased=False).mean())  # sklearn _tolerance
         labels = None
         for _ in range(self.kmeans_max_iter):
             dist_ = xx[:, None] - 2 * X @ C.t() + (C * C).sum(1)[None]

@@ -177,14 +177,15 @@ def make_table(counts_by_row, T, power=0.75):
     return out
 
 
-def community_train(x, pi, mu, inv, beta, lr, iters, chunksize=150):
-    """community_embeddings.py:61-78 restated over all rows (nodes = every vocab entry)."""
+def community_train(x, pi, mu, inv, beta, lr, iters, chunksize=150, rows=None):
+    """community_embeddings.py:61-78 restated; `rows` = the rows of `nodes` in order (default:
+    every vocab entry).  grad[ni] += bg is numpy's fancy-index add, as in the reference."""
     x = x.copy()
     V, K = pi.shape
-    idx_all = np.arange(V)
+    idx_all = np.arange(V) if rows is None else np.asarray(rows, np.int64)
     for _ in range(iters):
         grad = np.zeros(x.shape, np.float32)
-        for s in range(0, V, chunksize):
+        for s in range(0, len(idx_all), chunksize):
             ni = idx_all[s:s + chunksize]
             inp = x[ni]
             bg = np.zeros(inp.shape, np.float32)

@@ -85,3 +85,52 @@ def test_single_rank_sync_is_noop():
     before = t.clone()
     DeltaAllReduce([t]).sync()
     assert torch.equal(t, before)
+
+
+def _sparse_worker(rank, world, port, out_dir):
+    """The same training-like sequence through DeltaAllReduce and SparseDeltaAllReduce: each rank
+    changes a sparse, partly overlapping set of rows (some to -0.0, some touched then restored),
+    exchanges blocking and overlapped; both protocols must leave bit-identical tables."""
+    from come_amd.distributed import SparseDeltaAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.RandomState(7)
+    base = [rng.randn(200, 8).astype(np.float32), rng.randn(150, 16).astype(np.float32)]
+    base[0][3] = 0.0
+    results = []
+    for cls in (DeltaAllReduce, SparseDeltaAllReduce):
+        tables = [torch.from_numpy(b.copy()) for b in base]
+        sync = cls(tables, bucket_elems=64)
+        r2 = np.random.RandomState(50 + rank)
+        for step in range(4):
+            for t in tables:
+                rows = r2.choice(t.shape[0], 12, replace=False)
+                t[rows] += torch.from_numpy(r2.randn(12, t.shape[1]).astype(np.float32))
+            if step == 0:
+                tables[0][3] = -0.0                       # sign-only change is a change
+                tables[1][5] += 1.0
+                tables[1][5] -= 1.0                       # touched, maybe not restored exactly
+            if step % 2 == 0:
+                sync.sync()
+            else:
+                sync.start()
+                for t in tables:                          # progress during the exchange
+                    t[rank * 3:rank * 3 + 2] *= 1.5
+                sync.finish()
+        sync.sync()
+        if cls is SparseDeltaAllReduce:
+            assert 0 < sum(sync.last_rows) <= sum(t.shape[0] for t in tables)
+        results.append([t.numpy().copy() for t in tables])
+    for a, b in zip(results[0], results[1]):
+        assert np.array_equal(a.view(np.int32), b.view(np.int32)), rank
+    np.save(os.path.join(out_dir, "sparse_r%d.npy" % rank), results[1][0])
+    dist.destroy_process_group()
+
+
+def test_sparse_delta_allreduce_bit_identical_to_dense_world2(tmp_path):
+    world = 2
+    mp.spawn(_sparse_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r0 = np.load(os.path.join(str(tmp_path), "sparse_r0.npy"))
+    r1 = np.load(os.path.join(str(tmp_path), "sparse_r1.npy"))
+    np.testing.assert_array_equal(r0, r1)

@@ -366,6 +366,30 @@ def test_community_grad_vs_oracle(d, V, K, iters):
         np.testing.assert_allclose(x.cpu().numpy(), ref, rtol=2e-5, atol=2e-5)
 
 
+def test_community_train_node_subset_with_repeats():
+    """Community2Vec.train on a node list with repeats inside a chunk (counted once) and across
+    chunks (counted per chunk), as the reference's grad_input[node_index] += batch does."""
+    from come_amd.community_embeddings import Community2Vec
+    from come_amd.model import Model
+    rng = np.random.RandomState(8)
+    V, d, K = 300, 64, 3
+    np.random.seed(1)
+    m = Model((np.arange(1, V + 1), np.full(V, 2)), size=d, table_size=1000, k=K, device=DEV)
+    A = rng.normal(size=(K, d, d)) / np.sqrt(d)
+    inv = np.linalg.inv((np.einsum("kij,klj->kil", A, A) + 0.5 * np.eye(d)).astype(np.float32))
+    m.centroid = dev(rng.normal(size=(K, d)).astype(np.float32))
+    m.inv_covariance_mat = dev(inv.astype(np.float32))
+    m.pi = dev(rng.dirichlet(np.ones(K), V).astype(np.float32))
+    x0 = m.node_embedding.cpu().numpy()
+    nodes = list(rng.randint(1, V + 1, 90)) + [5, 5, 5, 7] + [5] * 3
+    cm = Community2Vec.__new__(Community2Vec)
+    cm.lr, cm.distributed, cm.group = 0.1, False, None
+    cm.train(nodes, m, 2.0, chunksize=10, iter=2)
+    ref = orc.community_train(x0, m.pi.cpu().numpy(), m.centroid.cpu().numpy(), inv, 2.0, 0.1, 2,
+                              chunksize=10, rows=np.array(nodes) - 1)
+    np.testing.assert_allclose(m.node_embedding.cpu().numpy(), ref, rtol=2e-5, atol=2e-5)
+
+
 def test_gmm_resp_vs_golden():
     z = np.load(os.path.join(GOLDEN, "gmm_resp.npz"))
     for name in z["names"]:

@@ -193,3 +193,13 @@ def test_graph_generators():
         if os.path.exists(os.path.join(GOLDEN, "karate.adjlist")) else (None, None)
     if g2 is not None:
         assert g2.V == 34 and g2.num_edges == 78
+
+
+def test_community_train_unknown_node_raises_keyerror():
+    """community_embeddings.py:64 looks nodes up with model.vocab[x]: an unknown id raises."""
+    from come_amd.community_embeddings import Community2Vec
+    m, _ = karate_model()
+    cm = Community2Vec.__new__(Community2Vec)
+    cm.lr, cm.distributed, cm.group = 0.1, False, None
+    with pytest.raises(KeyError):
+        cm.train([1, 2, 999], m, 0.01)
