@@ -50,7 +50,7 @@ def cpu_port_baseline(walks_np, seeds_np, node_np, ctx_np, table_np, window, neg
                       threads):
     """Time the builder's Hogwild C restatement of the reference's CPU path
     (oracle/come_oracle_mt.c: `threads` worker threads, one train_o2 walk per claim, plain racing
-    row updates -- context_embeddings.py:72-98 + pyx:454-509) on this host's cores.  The
+    row updates -- context_embeddings.py:72-102 + pyx:454-509) on this host's cores.  The
     reference itself never reaches the GPU box; the restatement's speed relative to the
     reference's Cython train_o2 driven by Python threads is measured in the container by
     scripts/calibrate_cpu.py (profiles/r02_cpu_calibration.json).  Returns (pairs/s, pairs,
@@ -316,8 +316,9 @@ def main():
         cpu = {"value": rate, "unit": "pair-updates/s", "cores": threads, "kind": "port",
                "nproc": orc.usable_cpus(), "visible_cpus": os.cpu_count(),
                "sample": "builder's Hogwild C restatement of the reference CPU path "
-                         "(oracle/come_oracle_mt.c, %s build): %d threads, one train_o2 walk per "
-                         "claim as Context2Vec's workers; %d walks / %d pair-updates of this "
+                         "(oracle/come_oracle_mt.c, %s build): %d threads taking jobs of 150 "
+                         "walks, one train_o2 per walk, as Context2Vec's workers; %d walks / %d "
+                         "pair-updates of this "
                          "workload (same graph, walks, seeds, tables, negative table) in %.1fs. "
                          "Calibration (profiles/r02_cpu_calibration.json, container, %s "
                          "threads): restatement / reference Cython train_o2 = %s" % (

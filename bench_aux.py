@@ -17,7 +17,6 @@ Each prints one JSON line.  CPU baselines: the reference's own code on a bounded
 Community2Vec.train loop restated in oracle/oracle.py and sklearn predict_proba).
 """
 import argparse
-import glob
 import json
 import os
 import sys
@@ -52,17 +51,6 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0), [a.elapsed_time(b) for a, b in ev]
 
 
-def ref_module():
-    import importlib.util
-    so = glob.glob(os.path.join(ROOT, "oracle", "_ref", "training_sdg_inner*.so"))
-    if not so:
-        return None
-    spec = importlib.util.spec_from_file_location("training_sdg_inner", so[0])
-    m = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(m)
-    return m
-
-
 def c2(args):
     import torch
     import come_amd.training_sdg_inner as tsi
@@ -79,49 +67,52 @@ def c2(args):
              for _ in range(args.steps + args.warmup)]
     it = iter(range(10 ** 9))
 
+    hot = m.hot_rows()  # the product's Hogwild launch (Node2Vec.train)
+    n_hot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
+
     def step():
         tsi.sgns_o1(m.node_embedding, edges, seeds[next(it) % len(seeds)], args.negative, m.table,
-                    0.2, tsi.MODE_HOGWILD)
+                    0.2, tsi.MODE_HOGWILD, hot=hot)
     el, ks = timed(step, args.steps, args.warmup)
     pairs = 2 * E
     n, d = args.negative, args.dim
     bpp = (3 + n) * d * 4
     avg = float(np.mean(ks)) / 1e3
     cpu = None
-    ref = ref_module()
-    if ref is not None and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
+        from oracle import oracle as orc
         node = m.node_embedding.cpu().numpy().copy()
-        table = m.table_host
-
-        class Vc(object):
-            __slots__ = ("index",)
-
-            def __init__(self, i):
-                self.index = i
-        items = [[Vc(int(u)), Vc(int(v))] for u, v in g.edges]
-        work = np.zeros(d, np.float32)
+        threads = orc.usable_cpus()
+        try:
+            o1_ratio = "%.1f" % json.load(open(os.path.join(
+                ROOT, "profiles", "r02_cpu_calibration.json")))["o1_ratio_restatement_over_cython"]
+        except (OSError, ValueError, KeyError):
+            o1_ratio = "n/a"
+        np.random.seed(98)
+        cs = tsi.draw_seeds(E)
         t0 = time.time()
-        done = 0
-        # Node2Vec.train is GIL-bound (one Python call per edge): one thread;
-        # passes over the edges until --cpu-seconds
+        done = pairs_done = 0
         while time.time() - t0 < args.cpu_seconds:
-            for e in items[done % len(items):]:
-                ref.train_o1(node, e, 0.2, n, table, py_size=d, py_work=work)
-                done += 1
-                if done % 4096 == 0 and time.time() - t0 > args.cpu_seconds:
-                    break
+            p, e = orc.sgns_o1_hogwild(node, g.edges.astype(np.int32), cs, n, m.table_host, 0.2,
+                                       threads, max(0.1, args.cpu_seconds - (time.time() - t0)))
+            pairs_done += p
+            done += e
         cel = time.time() - t0
-        cpu = {"value": 2 * done / cel, "unit": "pair-updates/s", "cores": 1,
-               "kind": "reference",
-               "sample": "reference Cython train_o1 (oracle/_ref), one call per edge as "
-                         "Node2Vec.train makes them (GIL-bound); %d edges in %.1fs" % (done, cel)}
+        cpu = {"value": pairs_done / cel, "unit": "pair-updates/s", "cores": threads,
+               "kind": "port",
+               "sample": "builder's Hogwild C restatement of train_o1 (oracle/come_oracle_mt.c), "
+                         "%d threads taking jobs of 150 edges; %d edges in %.1fs.  The "
+                         "reference's Node2Vec.train is GIL-bound (one Python call per edge): "
+                         "calibrated in the container, this restatement runs %s x the "
+                         "reference's Cython train_o1 at 8 threads "
+                         "(profiles/r02_cpu_calibration.json)" % (threads, done, cel, o1_ratio)}
     print(json.dumps({
         "metric": "O1 SGNS pair-updates/sec, SBM 100k nodes / 1M edges, d=128",
         "value": pairs * args.steps / el, "unit": "pair-updates/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True, "dtype": "f32", "data": "synthetic SBM (seed 0)",
         "config": {"workload": "configs[1]/C2: O1 over %d edges of a 100x1000 SBM, d=%d, "
-                               "negative=%d" % (E, d, n)},
+                               "negative=%d, lr=0.2" % (E, d, n), "hot_rows": n_hot},
         "roofline": {"bound": "hbm", "achieved": bpp * pairs / avg / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": bpp * pairs / avg / 1e9 / HBM_PEAK_GBS,
                      "bytes_per_pair": bpp, "avg_kernel_ms": avg * 1e3},

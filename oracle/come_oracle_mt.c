@@ -15,9 +15,11 @@
  *   /root/reference/utils/training_sdg_inner.pyx:105-151, :205-249 (fast0_o2 / fast0_o1)
  * Same per-pair arithmetic as come_oracle.c (pair enumeration, LCG draws, skip of a draw equal to
  * the positive, +-6 skip, EXP_TABLE bucket, g formula, sequential negative updates, in += work).
- * Granularity: one walk (edge) per claim from a shared counter -- the per-walk nogil call of the
- * reference -- so which thread runs which walk, and the interleaving of their row updates, is as
- * nondeterministic as the reference's worker pool.  Plain loads and stores on the shared tables,
+ * Granularity: a thread claims a job of `chunk` consecutive walks (edges) from a shared counter --
+ * the reference's job of `chunksize` items (context_embeddings.py:101-102, node_embeddings.py:
+ * 94-95, default 150) -- and runs one train_o2 (train_o1) per item, so which thread runs which
+ * walk, and the interleaving of their row updates, is as nondeterministic as the reference's
+ * worker pool.  Plain loads and stores on the shared tables,
  * as the reference's BLAS saxpy does (races are the algorithm).
  *
  * Dot product: eight float partial sums over the row (element i goes to sum i % 8), then the
@@ -191,6 +193,7 @@ typedef struct {
     uint64_t T;
     float lr, alpha;
     double deadline; /* 0 = none */
+    int64_t chunk;   /* items per claim (the reference's chunksize) */
     int64_t next;    /* shared claim counter (the reference's job queue) */
     int64_t pairs, done;
 } MtJob;
@@ -202,19 +205,22 @@ static void *mt_worker(void *arg) {
     const int path_len = j->L < MAX_SENTENCE_LEN ? j->L : MAX_SENTENCE_LEN; /* pyx:480 */
     for (;;) {
         if (j->deadline > 0.0 && now_s() > j->deadline) break;
-        const int64_t p = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
-        if (p >= j->count) break;
-        if (j->o2) {
-            pairs += mt_walk_o2(j->node, j->ctx, j->d, j->items + p * (int64_t)j->L, path_len,
-                                j->seeds[p], j->window, j->negative, j->table, j->T, j->lr,
-                                j->alpha, work, j->V);
-        } else {
-            const int32_t u = j->items[2 * p], v = j->items[2 * p + 1];
-            if (u >= 0 && v >= 0 && u < j->V && v < j->V)
-                pairs += mt_edge_o1(j->node, j->d, u, v, j->seeds[p], j->negative, j->table, j->T,
-                                    j->lr, work, j->V);
+        const int64_t p0 = __atomic_fetch_add(&j->next, j->chunk, __ATOMIC_RELAXED);
+        if (p0 >= j->count) break;
+        const int64_t p1 = p0 + j->chunk < j->count ? p0 + j->chunk : j->count;
+        for (int64_t p = p0; p < p1; ++p) {
+            if (j->o2) {
+                pairs += mt_walk_o2(j->node, j->ctx, j->d, j->items + p * (int64_t)j->L,
+                                    path_len, j->seeds[p], j->window, j->negative, j->table, j->T,
+                                    j->lr, j->alpha, work, j->V);
+            } else {
+                const int32_t u = j->items[2 * p], v = j->items[2 * p + 1];
+                if (u >= 0 && v >= 0 && u < j->V && v < j->V)
+                    pairs += mt_edge_o1(j->node, j->d, u, v, j->seeds[p], j->negative, j->table,
+                                        j->T, j->lr, work, j->V);
+            }
+            ++done;
         }
-        ++done;
     }
     free(work);
     __atomic_fetch_add(&j->pairs, pairs, __ATOMIC_RELAXED);
@@ -236,15 +242,16 @@ static int64_t mt_run(MtJob *j, int threads, int64_t *done_out) {
     return j->pairs;
 }
 
-/* Hogwild train_o2 over walks [P x L] (-1 = None) on `threads` threads.  max_seconds > 0 stops
- * claiming new walks after that long (walks already started finish).  Returns the pair updates
+/* Hogwild train_o2 over walks [P x L] (-1 = None) on `threads` threads, `chunk` walks per claim.
+ * max_seconds > 0 stops claiming new jobs after that long (jobs already claimed finish).  Returns the pair updates
  * performed; *walks_done = walks processed. */
 int64_t oracle_sgns_o2_hogwild(float *node, float *ctx, int64_t V, int d, const int32_t *walks,
                                int64_t P, int L, const uint64_t *seeds, int window, int negative,
                                const uint32_t *table, uint64_t T, float lr, float alpha,
-                               int threads, double max_seconds, int64_t *walks_done) {
-    MtJob j = {1,  node,   ctx,      V,     d, walks, P, L, seeds, window, negative, table, T, lr,
-               alpha, 0.0, 0, 0, 0};
+                               int threads, double max_seconds, int64_t chunk,
+                               int64_t *walks_done) {
+    MtJob j = {1,  node,   ctx,      V,     d,           walks, P, L, seeds, window, negative, table,
+               T,  lr,     alpha,    0.0,   chunk > 0 ? chunk : 1, 0, 0, 0};
     if (max_seconds > 0.0) j.deadline = now_s() + max_seconds;
     return mt_run(&j, threads, walks_done);
 }
@@ -252,10 +259,10 @@ int64_t oracle_sgns_o2_hogwild(float *node, float *ctx, int64_t V, int d, const 
 /* Hogwild train_o1 over edges [E x 2] on `threads` threads (same contract as above). */
 int64_t oracle_sgns_o1_hogwild(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
                                const uint64_t *seeds, int negative, const uint32_t *table,
-                               uint64_t T, float lr, int threads, double max_seconds,
+                               uint64_t T, float lr, int threads, double max_seconds, int64_t chunk,
                                int64_t *edges_done) {
-    MtJob j = {0, node, NULL, V, d, edges, E, 2, seeds, 0, negative, table, T, lr, 1.0f, 0.0,
-               0,    0,    0};
+    MtJob j = {0, node, NULL, V, d,   edges, E, 2, seeds, 0, negative, table, T, lr, 1.0f, 0.0,
+               chunk > 0 ? chunk : 1, 0,    0, 0};
     if (max_seconds > 0.0) j.deadline = now_s() + max_seconds;
     return mt_run(&j, threads, edges_done);
 }

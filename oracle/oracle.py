@@ -59,10 +59,10 @@ def lib():
         L.oracle_min_margin.restype = f64
         L.oracle_updates.restype = i64
         L.oracle_sgns_o2_hogwild.argtypes = [P, P, i64, i32, P, i64, i32, P, i32, i32, P, u64,
-                                             f32, f32, i32, f64, P]
+                                             f32, f32, i32, f64, i64, P]
         L.oracle_sgns_o2_hogwild.restype = i64
         L.oracle_sgns_o1_hogwild.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, f64,
-                                             P]
+                                             i64, P]
         L.oracle_sgns_o1_hogwild.restype = i64
         _lib = L
     return _lib
@@ -125,9 +125,9 @@ def sgns_o1(node, edges, seeds, negative, table, lr, dot_mode=DOT_REF):
 
 
 def sgns_o2_hogwild(node, ctx, walks, seeds, window, negative, table, lr, alpha, threads,
-                    max_seconds=0.0):
-    """Hogwild train_o2 on `threads` host threads, one walk per claim (come_oracle_mt.c,
-    context_embeddings.py:72-98).  Returns (pair updates, walks processed)."""
+                    max_seconds=0.0, chunk=150):
+    """Hogwild train_o2 on `threads` host threads, jobs of `chunk` walks (come_oracle_mt.c,
+    context_embeddings.py:72-102, chunksize default 150).  Returns (pair updates, walks)."""
     _chk(node, np.float32), _chk(ctx, np.float32), _chk(table, np.uint32)
     walks = np.ascontiguousarray(walks, np.int32)
     seeds = np.ascontiguousarray(seeds, np.uint64)
@@ -136,13 +136,15 @@ def sgns_o2_hogwild(node, ctx, walks, seeds, window, negative, table, lr, alpha,
     pairs = lib().oracle_sgns_o2_hogwild(_p(node), _p(ctx), node.shape[0], node.shape[1],
                                          _p(walks), walks.shape[0], walks.shape[1], _p(seeds),
                                          window, negative, _p(table), table.shape[0], lr, alpha,
-                                         int(threads), float(max_seconds), _p(done))
+                                         int(threads), float(max_seconds), int(chunk),
+                                         _p(done))
     return int(pairs), int(done[0])
 
 
-def sgns_o1_hogwild(node, edges, seeds, negative, table, lr, threads, max_seconds=0.0):
-    """Hogwild train_o1 on `threads` host threads, one edge per claim (node_embeddings.py:58-83).
-    Returns (pair updates, edges processed)."""
+def sgns_o1_hogwild(node, edges, seeds, negative, table, lr, threads, max_seconds=0.0,
+                    chunk=150):
+    """Hogwild train_o1 on `threads` host threads, jobs of `chunk` edges (node_embeddings.py:
+    58-95, chunksize default 150).  Returns (pair updates, edges processed)."""
     _chk(node, np.float32), _chk(table, np.uint32)
     edges = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
     seeds = np.ascontiguousarray(seeds, np.uint64)
@@ -150,7 +152,7 @@ def sgns_o1_hogwild(node, edges, seeds, negative, table, lr, threads, max_second
     pairs = lib().oracle_sgns_o1_hogwild(_p(node), node.shape[0], node.shape[1], _p(edges),
                                          edges.shape[0], _p(seeds), negative, _p(table),
                                          table.shape[0], lr, int(threads), float(max_seconds),
-                                         _p(done))
+                                         int(chunk), _p(done))
     return int(pairs), int(done[0])
 
 

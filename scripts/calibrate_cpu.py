@@ -100,6 +100,44 @@ def cython_leg(ref, walks, seeds, node, ctx, table, w, n, lr, seconds, threads):
     return state["pairs"] / el, state["pairs"], state["walks"], el
 
 
+def cython_o1_leg(ref, edges, node, table, n, lr, seconds, threads):
+    """Node2Vec.train-style driver of the reference's train_o1 (node_embeddings.py:58-83):
+    Python worker threads, one call per edge (GIL released only inside the call)."""
+
+    class Vocab(object):
+        __slots__ = ("index",)
+
+        def __init__(self, i):
+            self.index = i
+    items = [[Vocab(int(u)), Vocab(int(v))] for u, v in edges]
+    state = {"next": 0, "edges": 0}
+    lock = threading.Lock()
+    d = node.shape[1]
+    deadline = [0.0]
+
+    def worker():
+        work = np.zeros(d, np.float32)
+        while True:
+            with lock:
+                i = state["next"]
+                if i >= len(items) or time.time() > deadline[0]:
+                    return
+                state["next"] = i + 1
+            ref.train_o1(node, items[i], lr, n, table, py_size=d, py_work=work)
+            with lock:
+                state["edges"] += 1
+
+    ts = [threading.Thread(target=worker, daemon=True) for _ in range(threads)]
+    t0 = time.time()
+    deadline[0] = t0 + seconds
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.time() - t0
+    return 2 * state["edges"] / el, state["edges"], el
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
@@ -152,6 +190,25 @@ def main():
                                              "seconds": el}
             print(name, thr, "threads: %.3e pair-updates/s (%d walks in %.1fs)" % (
                 rate, done, el), flush=True)
+    # O1 (C2: SBM 100 x 1000, d=128, n=5, lr 0.2)
+    from come_amd.graph import sbm
+    g2 = sbm(100, 1000, 0.016, 4.04e-5, seed=0)
+    table2 = orc.make_table(g2.degree.astype(np.float64), args.table_size)
+    edges = g2.edges.astype(np.int32)
+    rng2 = np.random.RandomState(99)
+    node2 = rng2.uniform(-1, 1, (g2.V, d)).astype(np.float32)
+    eseeds = rng2.randint(0, 2 ** 48, len(edges), dtype=np.int64).astype(np.uint64)
+    for thr in sorted({1, args.threads}):
+        x = node2.copy()
+        t1 = time.time()
+        p, e = orc.sgns_o1_hogwild(x, edges, eseeds, 5, table2, 0.2, thr, args.seconds)
+        el = time.time() - t1
+        res["o1_restatement_%dthr" % thr] = {"pairs_per_s": p / el, "edges": e, "seconds": el}
+        x = node2.copy()
+        rate, e, el = cython_o1_leg(ref, edges, x, table2, 5, 0.2, args.seconds, thr)
+        res["o1_cython_%dthr" % thr] = {"pairs_per_s": rate, "edges": e, "seconds": el}
+        print("O1", thr, "threads: restatement %.3e, cython %.3e pair-updates/s" % (
+            res["o1_restatement_%dthr" % thr]["pairs_per_s"], rate), flush=True)
     k = args.threads
     out = {
         "what": "Hogwild C restatement (oracle/come_oracle_mt.c, bench.py cpu_baseline) vs the "
@@ -168,11 +225,17 @@ def main():
         / res["cython_%dthr" % k]["pairs_per_s"],
         "ratio_restatement_over_cython_1thr": res["restatement_1thr"]["pairs_per_s"]
         / res["cython_1thr"]["pairs_per_s"],
+        "o1_ratio_restatement_over_cython": res["o1_restatement_%dthr" % k]["pairs_per_s"]
+        / res["o1_cython_%dthr" % k]["pairs_per_s"],
+        "o1_workload": "C2: SBM 100x1000 (%d edges), d=128, negative=5, lr=0.2; the reference's "
+                       "Node2Vec.train is GIL-bound (one Python call per edge), the C "
+                       "restatement is not" % len(edges),
         "script": "scripts/calibrate_cpu.py",
     }
     json.dump(out, open(args.out, "w"), indent=1)
     print(json.dumps({k2: out[k2] for k2 in ("ratio_restatement_over_cython",
-                                             "ratio_restatement_over_cython_1thr")}))
+                                             "ratio_restatement_over_cython_1thr",
+                                             "o1_ratio_restatement_over_cython")}))
 
 
 if __name__ == "__main__":
