@@ -595,9 +595,6 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
 // chunks in a fixed order (deterministic, no float atomics).  blockIdx.x = k varies fastest, so
 // the K workgroups of one chunk run together and share its rows through L2 / MALL.
 constexpr int kCovRB = 64;
-constexpr int kCovAsyncRB = 32;  // k_gmm_cov_async: 2 x 16 KiB buffers keep 4 workgroups per CU
-constexpr int kCovKPB = 1;  // components per workgroup of k_gmm_cov_async (2 measured 13.4 ms vs
-                            // 11.4 ms at C4: profiles/r01h_ab_scatter_async.txt)
 
 struct CovArgs {
     const float *x;
@@ -620,6 +617,14 @@ struct CovShape {
     static constexpr int TPW = D == 128 ? 2 : 1;
     static constexpr int WAVES = NT / TPW;  // 5 (d = 128), 3 (d = 64)
     static_assert(NT % TPW == 0, "tiles must split evenly over the wavefronts");
+    // k_gmm_cov_async: CPW components per workgroup, 4 MFMA wavefronts (one per SIMD) with ATPW
+    // tiles each -- the CPW * NT tiles split evenly (2 x 10 = 4 x 5 at d = 128, 4 x 3 = 4 x 3 at
+    // 64) -- plus 4 staging wavefronts
+    static constexpr int AWAVES = 4;
+    static constexpr int ATHREADS = 2 * 64 * AWAVES;
+    static constexpr int CPW = D == 128 ? 2 : 4;
+    static constexpr int ATPW = CPW * NT / AWAVES;
+    static_assert(CPW * NT % AWAVES == 0, "async tiles must split evenly");
 };
 
 // tile t of the upper triangle (row-major over rt <= ct) -> (rt, ct)
@@ -698,110 +703,285 @@ __global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArg
     }
 }
 
-// Asynchronous form (default; "gmm_cov_async" = 0 selects k_gmm_cov_mfma): 11.40 vs 11.54 ms at
-// C4 with 32-row blocks (2 x 16 KiB buffers keep 4 workgroups per CU; 64-row blocks halved the
-// resident workgroups and ran 12.8 ms; profiles/r01h_ab_scatter_async.txt).  The
-// raw sample rows and their weights are copied global -> LDS by global_load_lds_dwordx4 into a
-// double buffer (64 rows x D, lane-linear 1 KiB pieces of the unpadded image; a half-wave's reads
-// of one row hit 32 consecutive banks), block b+1 in flight
-// while block b computes; the centring x - mu_k moves from the staging pass into the operand
-// reads (same fp32 subtraction, so the products are bit-identical to k_gmm_cov_mfma's).  Rows
-// past the chunk are clamped on the source side and get weight 0 at read time.
-template <int D, int KPB>
-__global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_async(CovArgs a) {
-    constexpr int CT = CovShape<D>::CT;
-    constexpr int TPW = CovShape<D>::TPW;
-    constexpr int WAVES = CovShape<D>::WAVES;
-    constexpr int XB = kCovAsyncRB * D;  // floats per row buffer
-    constexpr int PIECES = XB / 256;     // 1 KiB pieces per row buffer
-    static_assert(KPB * kCovAsyncRB <= 64, "one weight copy per block: KPB x rows <= 64 lanes");
+// The upper tiles T0 .. T0 + ATPW - 1 of one component (one MFMA wavefront's share), with the
+// distinct A-row and B-column tile indices they read, all at compile time.
+template <int D, int T0>
+struct CovTiles {
+    static constexpr int CT = CovShape<D>::CT;
+    static constexpr int N = CovShape<D>::ATPW;
+    static constexpr int rt(int t) {
+        int f = T0 + t, r = 0;
+        while (f >= CT - r) {
+            f -= CT - r;
+            ++r;
+        }
+        return r;
+    }
+    static constexpr int ct(int t) {
+        int f = T0 + t, r = 0;
+        while (f >= CT - r) {
+            f -= CT - r;
+            ++r;
+        }
+        return r + f;
+    }
+    // distinct values of rt (A) / ct (B) in order of first use; idx = position of tile t's
+    template <bool A>
+    static constexpr int val(int t) { return A ? rt(t) : ct(t); }
+    template <bool A>
+    static constexpr int count() {
+        int n = 0;
+        for (int t = 0; t < N; ++t) {
+            bool seen = false;
+            for (int u = 0; u < t; ++u) seen = seen || val<A>(u) == val<A>(t);
+            n += seen ? 0 : 1;
+        }
+        return n;
+    }
+    template <bool A>
+    static constexpr int nth(int i) {
+        int n = 0;
+        for (int t = 0; t < N; ++t) {
+            bool seen = false;
+            for (int u = 0; u < t; ++u) seen = seen || val<A>(u) == val<A>(t);
+            if (!seen) {
+                if (n == i) return val<A>(t);
+                ++n;
+            }
+        }
+        return -1;
+    }
+    template <bool A>
+    static constexpr int idx(int t) {
+        for (int i = 0; i < count<A>(); ++i)
+            if (nth<A>(i) == val<A>(t)) return i;
+        return -1;
+    }
+    struct Table {
+        int v[N];
+    };
+    template <bool A>
+    static constexpr Table idx_table() {
+        Table r{};
+        for (int t = 0; t < N; ++t) r.v[t] = idx<A>(t);
+        return r;
+    }
+};
+
+// NBUF image buffers: 3 -> one workgroup per CU, the MFMA wavefronts read a block's first
+// operands before the barrier that starts it; 2 -> two workgroups per CU (<= 128 registers per
+// wavefront), the other workgroup's MFMA wavefront covers each one's barrier.
+template <int D, int NBUF_>
+struct CovAsync {
+    static constexpr int RB = 32;                         // samples per block
+    static constexpr int LDT = RB + 4;                    // padded row of a transposed image
+    static constexpr int IMG = D * LDT;                   // floats per image
+    static constexpr int CPW = CovShape<D>::CPW;
+    static constexpr int WOFF = CPW * IMG;                // weights [CPW][RB] after the images
+    static constexpr int BUF = CPW * IMG + CPW * RB;      // floats per buffer
+    static constexpr int NBUF = NBUF_;
+    static constexpr int OPB = NBUF == 3 ? 2 : 1;         // operand register sets
+    static constexpr int WPE = NBUF == 3 ? 2 : 4;         // waves per SIMD the kernel is built for
+};
+
+// One MFMA wavefront over all nb blocks.  OPB == 2: operands of group g + 1 (or, NBUF == 3, of
+// the next block's group 0, staged two barriers earlier) are read while group g's MFMAs run.
+template <int D, int T0, int NBUF>
+__device__ __forceinline__ void cov_consume(const float *img, int nb, int tk, int lane,
+                                            __attribute__((ext_vector_type(16)))
+                                            float (&acc)[CovShape<D>::ATPW]) {
+    using TS = CovTiles<D, T0>;
+    using CA = CovAsync<D, NBUF>;
+    constexpr int OPB = CA::OPB;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int N = TS::N;
+    constexpr int NA = TS::template count<true>();
+    constexpr int NB = TS::template count<false>();
+    const int r = lane & 31, h = lane >> 5;
+    int ab[NA], bb[NB];
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+        ab[i] = tk * CA::IMG + (TS::template nth<true>(i) * 32 + r) * CA::LDT + 4 * h;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+        bb[i] = tk * CA::IMG + (TS::template nth<false>(i) * 32 + r) * CA::LDT + 4 * h;
+    const int wb = CA::WOFF + tk * CA::RB + 4 * h;
+    constexpr typename TS::Table IA = TS::template idx_table<true>();
+    constexpr typename TS::Table IB = TS::template idx_table<false>();
+    f32x4 ra[OPB][NA], rb[OPB][NB], rw[OPB];
+    auto fetch = [&](int blk, int g, int slot) {
+        const float *buf = img + (blk % CA::NBUF) * CA::BUF + 8 * g;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) ra[slot][i] = *reinterpret_cast<const f32x4 *>(buf + ab[i]);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) rb[slot][i] = *reinterpret_cast<const f32x4 *>(buf + bb[i]);
+        rw[slot] = *reinterpret_cast<const f32x4 *>(buf + wb);
+    };
+    for (int j = 0; j < nb; ++j) {
+        if (NBUF == 2 || j == 0) {
+            __syncthreads();  // barrier j: block j staged
+            fetch(j, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < CA::RB / 8; ++g) {
+            const int cur = OPB == 2 ? (g & 1) : 0;  // RB / 8 is even: group 0 is slot 0
+            if (OPB == 2) {
+                if (g + 1 < CA::RB / 8) fetch(j, g + 1, cur ^ 1);
+                else if (NBUF == 3 && j + 1 < nb) fetch(j + 1, 0, cur ^ 1);
+            }
+            f32x4 wa[NA];  // A = r * (x - mu), the synchronous form's product
+#pragma unroll
+            for (int i = 0; i < NA; ++i) wa[i] = rw[cur] * ra[cur][i];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int t = 0; t < N; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                        wa[IA.v[t]][q], rb[cur][IB.v[t]][q], acc[t], 0, 0, 0);
+            if (OPB == 1 && g + 1 < CA::RB / 8) fetch(j, g + 1, 0);
+        }
+        if (NBUF == 3 && j + 1 < nb) __syncthreads();  // barrier j + 1
+    }
+}
+
+// Default form ("gmm_cov_async" = 0 selects the synchronous k_gmm_cov_mfma).  What limited the
+// earlier forms (SQ counters at C4, profiles/r01h_c4_pmc_sq.txt, profiles/r02_c4_scatter_ab.txt):
+// VALU work per MFMA (every operand centred and weighted at read time: 8.6 VALU per MFMA), SIMD
+// imbalance (5-wavefront workgroups put two tile sets on one SIMD of four), MFMA wavefronts
+// stopping to stage each block, and sample loads landing later than one block period.  Here:
+//  * CPW components per workgroup (2 at d = 128, 4 at d = 64): the CPW x NT upper tiles split
+//    exactly over 4 MFMA wavefronts (ATPW each, one per SIMD), and the components share one
+//    global read of each sample block;
+//  * 4 more wavefronts only stage: a 32-sample block is loaded global -> VGPRs three blocks
+//    ahead, centred once per component into a transposed LDS image B[k][c][s] = x_s[c] - mu_k[c]
+//    (rows padded to 36 floats) and its weights r_sk stored beside it.  The MFMA wavefronts form
+//    A = r_sk * B[k][c][s] in registers (the synchronous form's fp32 subtraction and product:
+//    every MFMA operand is bit-identical), 4 VALU per distinct A row per 20 MFMAs;
+//  * image buffers: NBUF = 2 (default) -> block j + 1 is staged while block j is multiplied,
+//    74 KB, two workgroups per CU whose MFMA wavefronts cover each other's barriers; NBUF = 3 ->
+//    111 KB, one workgroup per CU that reads the next block's first operands before its barrier.
+//    One barrier per block either way;
+//  * the k-steps pair samples s(q, h) = 8 (q/4) + 4 h + q%4, so the four consecutive k-steps of
+//    a lane read one 16-byte group of a row: one ds_read_b128 per distinct operand row per 4
+//    MFMAs (6 or 5 rows for a wavefront's 5 tiles at d = 128), and the padding sends the 16
+//    lanes of each b128 phase to 16 distinct 4-bank groups.
+// C4 (V = 1M, K = 50, d = 128): 7.9 ms (NBUF 2) / 8.7 ms (NBUF 3) vs 11.3 ms for round 1's form.
+template <int D, int NBUF>
+__global__ void __launch_bounds__(CovShape<D>::ATHREADS)
+    __attribute__((amdgpu_waves_per_eu(CovAsync<D, NBUF>::WPE))) k_gmm_cov_async(CovArgs a) {
+    using CA = CovAsync<D, NBUF>;
+    constexpr int NT = CovShape<D>::NT;
+    constexpr int CPW = CA::CPW;
+    constexpr int TPW = CovShape<D>::ATPW;
+    constexpr int NST = 64 * CovShape<D>::AWAVES;  // staging threads
+    constexpr int RB = CA::RB;
+    constexpr int SPT = RB * D / NST;  // samples staged per thread (16 at d = 128, 8 at d = 64)
     using f32x16 = __attribute__((ext_vector_type(16))) float;
-    extern __shared__ __attribute__((aligned(16))) float smc[];  // [2][XB] rows, [2][64] weights
-    const int kb = blockIdx.x * KPB;  // components kb .. kb + KPB - 1 share the staged rows
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    static_assert(SPT % 4 == 0 && SPT * CPW <= 64 && D % 64 == 0, "staging layout");
+    static_assert(CA::NBUF * CA::BUF * sizeof(float) <= 160 * 1024, "LDS budget");
+    static_assert(TPW <= NT && NT % TPW == 0, "a wavefront's tiles lie in one component");
+    __shared__ __attribute__((aligned(16))) float img[CA::NBUF * CA::BUF];
+    const int k0 = blockIdx.x * CPW;
+    const int nk = a.K - k0 < CPW ? a.K - k0 : CPW;
     const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
     int64_t c1 = c0 + a.rows_per_chunk;
     if (c1 > a.V) c1 = a.V;
-    const int tid = threadIdx.x;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int r = lane & 31, h = lane >> 5;
-    int rts[TPW], cts[TPW];
-    float mr[KPB][TPW], mc[KPB][TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        upper_tile(wid * TPW + t, CT, rts[t], cts[t]);
-#pragma unroll
-        for (int j = 0; j < KPB; ++j) {
-            const int k = kb + j < a.K ? kb + j : a.K - 1;
-            mr[j][t] = a.means[k * D + rts[t] * 32 + r];
-            mc[j][t] = a.means[k * D + cts[t] * 32 + r];
-        }
-    }
-    f32x16 acc[KPB][TPW];
-#pragma unroll
-    for (int j = 0; j < KPB; ++j)
+    const int nb = c1 > c0 ? (int)((c1 - c0 + RB - 1) / RB) : 0;
+    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wid < CovShape<D>::AWAVES) {
+        // ---- MFMA wavefronts: component tk, tiles t0 .. t0 + TPW - 1 ----
+        const int tk = wid * TPW / NT, t0 = wid * TPW % NT;
+        f32x16 acc[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.0f;
-    auto stage = [&](int64_t b, int buf) {
-        for (int i = wid; i < PIECES; i += WAVES) {
-            const int f = i * 256 + lane * 4;    // float offset in the row buffer
-            int64_t row = b + f / D;
-            if (row >= c1) row = c1 - 1;
-            __builtin_amdgcn_global_load_lds(a.x + row * D + f % D, smc + buf * XB + i * 256, 16,
-                                             0, 0);
+            for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+        if (nb > 0) {
+            if (t0 == 0) cov_consume<D, 0, NBUF>(img, nb, tk, lane, acc);
+            else cov_consume<D, (NT == TPW ? 0 : TPW), NBUF>(img, nb, tk, lane, acc);
         }
-        if (wid == WAVES - 1) {  // lane = j * 32 + s: weight of sample s for component kb + j
-            const int j = lane / kCovAsyncRB;
-            const int k = kb + j < a.K ? kb + j : a.K - 1;
-            int64_t row = b + lane % kCovAsyncRB;
-            if (row >= c1) row = c1 - 1;
-            __builtin_amdgcn_global_load_lds(a.resp + row * a.K + k, smc + 2 * XB + buf * 64, 4,
-                                             0, 0);
-        }
-    };
-    if (c0 < c1) stage(c0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int buf = 0;
-    for (int64_t b = c0; b < c1; b += kCovAsyncRB, buf ^= 1) {
-        if (b + kCovAsyncRB < c1) stage(b + kCovAsyncRB, buf ^ 1);
-        const float *xb = smc + buf * XB;
-        const float *wb = smc + 2 * XB + buf * 64;
-#pragma unroll 4
-        for (int s0 = 0; s0 < kCovAsyncRB; s0 += 2) {
-            const int sr = s0 + h;
-            const float *row = xb + sr * D;
-            const bool ok = b + sr < c1;
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) {
-                const float xr = row[rts[t] * 32 + r], xc = row[cts[t] * 32 + r];
-#pragma unroll
-                for (int j = 0; j < KPB; ++j) {
-                    const float w = ok ? wb[j * kCovAsyncRB + sr] : 0.0f;
-                    const float av = w * (xr - mr[j][t]);
-                    const float bv = xc - mc[j][t];
-                    acc[j][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j][t], 0, 0, 0);
-                }
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // block b+1 landed; every wavefront is done with block b
-    }
-#pragma unroll
-    for (int j = 0; j < KPB; ++j) {
-        if (kb + j >= a.K) break;
-        float *out = a.out + ((int64_t)blockIdx.y * a.K + kb + j) * D * D;
+        if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+        const int r = lane & 31, h = lane >> 5;
+        float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            const int rt = rts[t], ct = cts[t];
+            int rt, ct;
+            upper_tile(t0 + t, CovShape<D>::CT, rt, ct);
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int ii = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 const int jj = ct * 32 + r;
-                out[(int64_t)i * D + jj] = acc[j][t][e];
-                if (rt != ct) out[(int64_t)jj * D + i] = acc[j][t][e];
+                out[(int64_t)ii * D + jj] = acc[t][e];
+                if (rt != ct) out[(int64_t)jj * D + ii] = acc[t][e];
             }
+        }
+        return;
+    }
+    // ---- staging wavefronts: thread owns column sc and samples SPT sp .. SPT sp + SPT - 1 of a
+    // block (sp uniform over a wavefront); lane l < SPT * CPW also carries the weight of sample
+    // SPT sp + l % SPT for component k0 + l / SPT ----
+    const int st = tid - NST;
+    const int sc = st % D, sp = st / D;
+    float mu[CPW];
+#pragma unroll
+    for (int kk = 0; kk < CPW; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
+    // block b's samples and weight live in register set b % 3: loads run 3 blocks ahead of the
+    // stage that consumes them (an HBM / MALL round trip under load exceeds one block period)
+    float xv[3][SPT];
+    float wl[3];
+    const int wk = lane / SPT, ws = lane % SPT;
+    const bool wlane = lane < SPT * CPW;
+    auto load = [&](int blk, float (&xr)[SPT], float &wr) {
+        const int64_t b = c0 + (int64_t)blk * RB;
+        const float *src = a.x + (b + SPT * sp) * D + sc;
+        if (b + RB <= c1) {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) xr[q] = src[q * D];
+        } else {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) xr[q] = b + SPT * sp + q < c1 ? src[q * D] : 0.0f;
+        }
+        const int64_t wrow = b + SPT * sp + ws;
+        wr = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
+    };
+    auto stage = [&](int blk, const float (&xr)[SPT], float wr) {
+        float *buf = img + (blk % CA::NBUF) * CA::BUF;
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+            for (int j = 0; j < SPT / 4; ++j) {
+                f32x4 xb;
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) xb[q4] = xr[4 * j + q4] - mu[kk];
+                *reinterpret_cast<f32x4 *>(buf + kk * CA::IMG + sc * CA::LDT + SPT * sp + 4 * j) =
+                    xb;
+            }
+        if (wlane) buf[CA::WOFF + wk * RB + SPT * sp + ws] = wr;
+    };
+    if (nb == 0) return;
+    constexpr int SD = NBUF - 1;  // block j + SD is staged while block j is multiplied
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+        if (u < nb) load(u, xv[u], wl[u]);
+#pragma unroll
+    for (int u = 0; u < SD; ++u)
+        if (u < nb) {
+            stage(u, xv[u], wl[u]);
+            if (u + 3 < nb) load(u + 3, xv[u], wl[u]);
+        }
+    __syncthreads();  // barrier 0
+    for (int j0 = 0; j0 < nb; j0 += 3) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {  // j = j0 + u, j0 % 3 == 0: register set (j + SD) % 3
+            const int j = j0 + u;
+            if (j >= nb) break;
+            if (j + SD < nb) {
+                // buffer (j + SD) % NBUF = (j - 1) % NBUF: block j - 1 finished at barrier j
+                stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+                if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+            }
+            if (j + 1 < nb) __syncthreads();  // barrier j + 1
         }
     }
 }
@@ -1192,24 +1372,16 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const bool cov_async = current_opts().gmm_cov_async != 0;
     void (*kern)(CovArgs) =
         !mfma ? k_gmm_cov_valu
-              : cov_async ? (d == 64 ? k_gmm_cov_async<64, kCovKPB>
-                                       : k_gmm_cov_async<128, kCovKPB>)
+              : cov_async ? (current_opts().gmm_cov_async == 2
+                                 ? (d == 64 ? k_gmm_cov_async<64, 3> : k_gmm_cov_async<128, 3>)
+                                 : (d == 64 ? k_gmm_cov_async<64, 2> : k_gmm_cov_async<128, 2>))
                             : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
-    const int threads = !mfma ? 256 : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
-    size_t lds = 0;
-    if (mfma && cov_async) {
-        lds = sizeof(float) * (size_t)(2 * kCovAsyncRB * d + 2 * 64);
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<64, kCovKPB>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_gmm_cov_async<128, kCovKPB>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
-    }
-    const unsigned gx = (mfma && cov_async) ? (unsigned)((K + kCovKPB - 1) / kCovKPB) : K;
-    hipLaunchKernelGGL(kern, dim3(gx, used), dim3(threads), lds, (hipStream_t)stream, a);
+    const int threads = !mfma      ? 256
+                        : cov_async ? CovShape<128>::ATHREADS
+                                    : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
+    const int cpw = !mfma || !cov_async ? 1 : d == 64 ? CovShape<64>::CPW : CovShape<128>::CPW;
+    hipLaunchKernelGGL(kern, dim3((K + cpw - 1) / cpw, used), dim3(threads), 0,
+                       (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;
     hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
