@@ -220,7 +220,9 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
 
 /* ---- Launch options ----
  * Kernel-selection and grid knobs (0 = automatic unless stated):
- *   o2_kernel           1 = direct kernel, 2 = LDS-ring kernel (automatic: ring when it fits)
+ *   o2_kernel           1 = direct kernel, 2 = LDS-ring kernel, 3 = streaming kernel.  Automatic:
+ *                       sequential -> ring when it fits; Hogwild -> streaming when the vocabulary
+ *                       has >= 32 rows per wavefront in flight (and window <= 31), else direct
  *   o2_blocks_per_cu    O2 grid cap in workgroups per CU
  *   o2_waves_per_block  1 or 2 (automatic 2)
  *   o2_static           1 = static grid-stride walk assignment instead of the device work queue

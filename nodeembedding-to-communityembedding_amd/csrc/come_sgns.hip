@@ -10,6 +10,7 @@
 namespace come {
 
 constexpr size_t kRingMaxWaveBytes = 40 * 1024;
+constexpr int64_t kStreamRowsPerWave = 32;  // automatic Hogwild O2 kernel choice (come_sgns_o2_ex)
 
 // Cap on the number of workgroups of a Hogwild launch (0 = none).
 // Launch knobs come from the caller's come_launch_opts or one snapshot of the process-wide ones
@@ -140,17 +141,30 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
     const KernelSet &ks = kernel_set(d, &full);
     const int mi = maxn_index(negative);
     const bool hog = mode == COME_MODE_HOGWILD;
-    if (hog && o.o2_kernel != 1 && window <= 31) {
+    if (hog && (o.o2_kernel == 0 || o.o2_kernel == 3) && window <= 31) {
         // streaming Hogwild kernel: 4-wave workgroups, 8 per CU (= its 8 waves per SIMD at
         // d <= 128, n <= 5; measured 6 / 7 / 8 -> 122 / 115 / 108 ms per C3 launch), device work
         // queue
         int dev = 0;
         rc = ensure_init(&dev);
         if (rc) return rc;
-        if (!o.o2_static) a.counter = launch_counter(dev, stream);  // else grid-stride
-        return launch(o, ks.o2_stream[full][mi], &a, P, mode, 4,
-                      o.o2_blocks_per_cu > 0 ? o.o2_blocks_per_cu : 8, 0, stream,
-                      hog_max_blocks(o, V, 4, o.rows_per_wave));
+        const int bpc = o.o2_blocks_per_cu > 0 ? o.o2_blocks_per_cu : 8;
+        const int64_t hcap = hog_max_blocks(o, V, 4, o.rows_per_wave);
+        int64_t blocks = (P + 3) / 4;
+        if (blocks > (int64_t)num_cus(dev) * bpc) blocks = (int64_t)num_cus(dev) * bpc;
+        if (hcap > 0 && blocks > hcap) blocks = hcap;
+        // Automatic choice: the streaming kernel reads each pair's rows one pair ahead and runs
+        // 1.4x the direct kernel's pair rate, so a hub row collects that many more concurrent
+        // updates computed from a stale copy.  With fewer than kStreamRowsPerWave rows per
+        // wavefront in flight that occasionally throws a hub's node row into the +-6 skip region
+        // for good (100k-node Chung-Lu, 10k walks: held-out loss +3..7% in 2-4 of 10 launches;
+        // none at 200k-1M nodes; profiles/r02_ab_hogwild_contention.txt), so small vocabularies
+        // run the direct kernel, which reads every row when its pair starts (stable in every
+        // run, the same speed there: nearly every row is hot and atomic-bound).
+        if (o.o2_kernel == 3 || V >= kStreamRowsPerWave * 4 * blocks) {
+            if (!o.o2_static) a.counter = launch_counter(dev, stream);  // else grid-stride
+            return launch(o, ks.o2_stream[full][mi], &a, P, mode, 4, bpc, 0, stream, hcap);
+        }
     }
     // LDS ring of the sequential kernel: (2w+1) rows + their ids
     const int rs = 2 * window + 1;

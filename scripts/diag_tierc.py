@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--nodes", type=int, default=100000)
     ap.add_argument("--variants", default="")
     ap.add_argument("--hot-p", default="1e-3,1e-4,3e-5,1e-5,3e-6")
+    ap.add_argument("--waves", default="1024", help="max_waves values for hot_p<p>_w<waves>")
+    ap.add_argument("--repeat", type=int, default=1, help="runs per variant (Hogwild spread)")
+    ap.add_argument("--no-oracle", action="store_true", help="skip the sequential C oracle")
     args = ap.parse_args()
     import torch
     import come_amd.training_sdg_inner as tsi
@@ -58,14 +61,21 @@ def main():
     for p in args.hot_p.split(","):
         variants["hot_p%s" % p] = (tsi.MODE_HOGWILD, {"_hot_p": float(p)})
         variants["direct_hot_p%s" % p] = (tsi.MODE_HOGWILD, {"o2_kernel": 1, "_hot_p": float(p)})
-        variants["hot_p%s_w1024" % p] = (tsi.MODE_HOGWILD, {"max_waves": 1024, "_hot_p": float(p)})
+        variants["stream_hot_p%s" % p] = (tsi.MODE_HOGWILD, {"o2_kernel": 3, "_hot_p": float(p)})
+        for mw in args.waves.split(","):
+            variants["hot_p%s_w%s" % (p, mw)] = (tsi.MODE_HOGWILD, {"max_waves": int(mw),
+                                                                     "_hot_p": float(p)})
     if args.variants:
         variants = {k: v for k, v in variants.items() if k in args.variants.split(",")}
     out = {"init": l0}
-    sn, sc = node0.copy(), np.zeros_like(node0)
-    orc.sgns_o2_hogwild(sn, sc, train, seeds, w, n, table, lr, 1.0, threads=1)
-    out["oracle_seq"] = sgns_loss(sn, sc, ri, rp, rn)
-    for name, (mode, opts) in variants.items():
+    if not args.no_oracle:
+        sn, sc = node0.copy(), np.zeros_like(node0)
+        orc.sgns_o2_hogwild(sn, sc, train, seeds, w, n, table, lr, 1.0, threads=1)
+        out["oracle_seq"] = sgns_loss(sn, sc, ri, rp, rn)
+        print("oracle_seq", out["oracle_seq"], flush=True)
+    runs = [(name, r) for name in variants for r in range(args.repeat)]
+    for name, rep in runs:
+        mode, opts = variants[name]
         opts = dict(opts)
         hp = opts.pop("_hot_p", None)
         hot = None
@@ -83,11 +93,12 @@ def main():
         loss = sgns_loss(hn, hc, ri, rp, rn) if fin else float("nan")
         hub = int(np.argmax(g.degree))
         nhot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
-        out[name] = {"loss": loss, "ms": el * 1e3, "hot_rows": nhot,
+        key = name if args.repeat == 1 else "%s#%d" % (name, rep)
+        out[key] = {"loss": loss, "ms": el * 1e3, "hot_rows": nhot,
                      "hub_node_norm": float(np.linalg.norm(hn[hub])),
                      "hub_ctx_norm": float(np.linalg.norm(hc[hub])),
                      "max_ctx_norm": float(np.linalg.norm(hc, axis=1).max())}
-        print(name, json.dumps(out[name]), flush=True)
+        print(key, json.dumps(out[key]), flush=True)
     print(json.dumps(out))
 
 

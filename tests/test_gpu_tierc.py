@@ -85,43 +85,107 @@ def c3_shape():
     return g, table, walks[:10_000], walks[10_000:], node0, seeds
 
 
-def test_o2_hogwild_heldout_loss_matches_sequential_oracle(c3_shape):
-    g, table, train, held, node0, seeds = c3_shape
+def o2_tierc(g, table, train, held, node0, seeds, runs=3, cpu=True):
+    """Held-out loss of `runs` GPU Hogwild launches (the product's launch: Context2Vec.train's
+    hot-row bitmap, the automatic kernel choice) against the sequential oracle, the same walks
+    reversed (the ordering effect alone) and the reference's regime (Hogwild C threads)."""
     w, n, lr = 5, 5, 0.1
     rows_in, rows_pos, rows_neg = heldout_o2_pairs(held, w, n, table, 200_000, 24)
     ctx0 = np.zeros_like(node0)
     l0 = sgns_loss(node0, ctx0, rows_in, rows_pos, rows_neg)
-
-    node, ctx = dev(node0), dev(ctx0)
-    tab = dev(table)
-    # the product's Hogwild launch (Context2Vec.train): contended rows from the table
+    tab, tw, ts = dev(table), dev(train), dev(seeds)
     hot = tsi.hot_rows(tab, g.V, int(tsi.DEFAULT_HOT_P * len(table)))
-    tsi.sgns_o2(node, ctx, dev(train), dev(seeds), w, n, tab, lr, 1.0, tsi.MODE_HOGWILD, hot=hot)
-    torch.cuda.synchronize()
-    hn, hc = node.cpu().numpy(), ctx.cpu().numpy()
-    assert np.isfinite(hn).all() and np.isfinite(hc).all()
-    l_hog = sgns_loss(hn, hc, rows_in, rows_pos, rows_neg)
-
+    l_hog = []
+    for _ in range(runs):  # Hogwild is not reproducible: every launch must pass, not one
+        node, ctx = dev(node0), dev(ctx0)
+        tsi.sgns_o2(node, ctx, tw, ts, w, n, tab, lr, 1.0, tsi.MODE_HOGWILD, hot=hot)
+        torch.cuda.synchronize()
+        hn, hc = node.cpu().numpy(), ctx.cpu().numpy()
+        assert np.isfinite(hn).all() and np.isfinite(hc).all()
+        l_hog.append(sgns_loss(hn, hc, rows_in, rows_pos, rows_neg))
     sn, sc = node0.copy(), ctx0.copy()
     pairs, done = orc.sgns_o2_hogwild(sn, sc, train, seeds, w, n, table, lr, 1.0, threads=1)
     assert done == len(train)
     l_seq = sgns_loss(sn, sc, rows_in, rows_pos, rows_neg)
-    # the ordering effect alone: the same walks (same seeds per walk) in reversed order
     rn, rc = node0.copy(), ctx0.copy()
     orc.sgns_o2_hogwild(rn, rc, train[::-1].copy(), seeds[::-1].copy(), w, n, table, lr, 1.0,
                         threads=1)
     l_rev = sgns_loss(rn, rc, rows_in, rows_pos, rows_neg)
-    # the reference's own regime: Hogwild C threads on the host
-    cn, cc = node0.copy(), ctx0.copy()
-    orc.sgns_o2_hogwild(cn, cc, train, seeds, w, n, table, lr, 1.0,
-                        threads=min(16, orc.usable_cpus()))
-    l_cpu = sgns_loss(cn, cc, rows_in, rows_pos, rows_neg)
-    rel = abs(l_hog - l_seq) / l_seq
-    print("O2 held-out loss: init %.5f  seq %.5f  reversed %.5f  cpu-hogwild %.5f  "
-          "gpu-hogwild %.5f  |gpu-seq|/seq %.5f  |rev-seq|/seq %.5f" % (
-              l0, l_seq, l_rev, l_cpu, l_hog, rel, abs(l_rev - l_seq) / l_seq))
+    l_cpu = float("nan")
+    if cpu:
+        cn, cc = node0.copy(), ctx0.copy()
+        orc.sgns_o2_hogwild(cn, cc, train, seeds, w, n, table, lr, 1.0,
+                            threads=min(16, orc.usable_cpus()))
+        l_cpu = sgns_loss(cn, cc, rows_in, rows_pos, rows_neg)
+    rel = [abs(x - l_seq) / l_seq for x in l_hog]
+    print("O2 held-out loss (V=%d, %d walks, %d pairs): init %.5f  seq %.5f  reversed %.5f  "
+          "cpu-hogwild %.5f  gpu-hogwild %s  max |gpu-seq|/seq %.5f  |rev-seq|/seq %.5f" % (
+              g.V, len(train), pairs, l0, l_seq, l_rev, l_cpu,
+              " ".join("%.5f" % x for x in l_hog), max(rel), abs(l_rev - l_seq) / l_seq))
     assert l_seq < l0 - 0.05  # training moved the loss: the comparison is not vacuous
-    assert rel < 0.01, (l_hog, l_seq)  # SURVEY.md §8c tier C
+    assert max(rel) < 0.01, (l_hog, l_seq)  # SURVEY.md §8c tier C, every launch
+
+
+def test_o2_hogwild_heldout_loss_matches_sequential_oracle(c3_shape):
+    """100k nodes, 10k walks in one launch: every walk in flight at once, the most contended
+    regime (the automatic choice runs the direct kernel here, come_sgns_o2_ex)."""
+    o2_tierc(*c3_shape)
+
+
+C3_FIXTURE = os.path.join(GOLDEN, "tierc_c3_seq.json")
+
+
+def c3_vocab_inputs(walks_n=131_072):
+    """The benchmarked shape (configs[2]/C3): Chung-Lu 1M nodes (gamma 2.5, mean degree 20,
+    bench.py's seed), T = 1e8, d=128, n=5, w=5, L=80, lr 0.1, and ONE bench launch of training
+    walks (131,072, from the device walker); 20,000 held-out walks."""
+    import hashlib
+    from come_amd.graph import chung_lu, random_walks
+    g = chung_lu(1_000_000, 20.0, gamma=2.5, seed=1)
+    table = orc.make_table(g.degree.astype(np.float64), 100_000_000)
+    walks = random_walks(g, 1, 80, seed=100, device="cuda")
+    rng = np.random.RandomState(7)
+    pick = torch.from_numpy(rng.choice(walks.shape[0], walks_n + 20000, replace=False))
+    walks = walks[pick.to(walks.device)].cpu().numpy()
+    node0 = rng.uniform(-1, 1, (g.V, 128)).astype(np.float32)
+    seeds = rng.randint(0, 2 ** 48, walks_n, dtype=np.int64).astype(np.uint64)
+    digest = hashlib.sha256(walks.tobytes() + table.tobytes()[:1 << 20]).hexdigest()
+    return g, table, walks[:walks_n], walks[walks_n:], node0, seeds, digest
+
+
+def test_o2_hogwild_heldout_loss_at_benchmarked_shape():
+    """Tier C at C3 itself: one bench launch (131,072 walks, 1.0e8 pair updates) of the product's
+    Hogwild path (streaming kernel) against the sequential oracle's held-out loss after the same
+    walks.  The oracle run takes ~3 minutes on one core, so its result is a committed fixture
+    (tests/golden/tierc_c3_seq.json, scripts/make_tierc_fixture.py: the same inputs, sequential C
+    oracle in walk order); the inputs' digest must match it.  Measured (profiles/
+    r02_tierc_vs_walks_c3_vocab.json): the gap is 2.2% after 16k walks, 0.6% after 49k and
+    < 0.1% after this launch -- the GPU's thousands of walks in flight act like a large minibatch
+    early on, and the effect fades as training proceeds."""
+    import json
+    fx = json.load(open(C3_FIXTURE))
+    g, table, train, held, node0, seeds, digest = c3_vocab_inputs(fx["walks"])
+    assert digest == fx["inputs_sha256"], "inputs differ from the fixture's (walker / graph changed)"
+    w, n, lr = 5, 5, 0.1
+    rows_in, rows_pos, rows_neg = heldout_o2_pairs(held, w, n, table, 200_000, 24)
+    l0 = sgns_loss(node0, np.zeros_like(node0), rows_in, rows_pos, rows_neg)
+    assert abs(l0 - fx["init_loss"]) < 1e-9
+    tab = dev(table)
+    hot = tsi.hot_rows(tab, g.V, int(tsi.DEFAULT_HOT_P * len(table)))
+    l_hog = []
+    for _ in range(2):
+        node = dev(node0)
+        ctx = torch.zeros_like(node)
+        tsi.sgns_o2(node, ctx, dev(train), dev(seeds), w, n, tab, lr, 1.0, tsi.MODE_HOGWILD,
+                    hot=hot)
+        torch.cuda.synchronize()
+        l_hog.append(sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), rows_in, rows_pos,
+                               rows_neg))
+    rel = [abs(x - fx["seq_loss"]) / fx["seq_loss"] for x in l_hog]
+    print("C3 held-out loss: init %.5f  seq (fixture) %.5f  gpu-hogwild %s  max rel %.5f" % (
+        l0, fx["seq_loss"], " ".join("%.5f" % x for x in l_hog), max(rel)))
+    assert fx["seq_loss"] < l0 - 0.5
+    assert max(rel) < 0.01, (l_hog, fx["seq_loss"])  # SURVEY.md §8c tier C
 
 
 def test_o2_update_count_matches_oracle(c3_shape):
