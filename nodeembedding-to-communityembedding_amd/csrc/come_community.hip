@@ -100,6 +100,7 @@ struct RespArgs {
     int d;
     int K;
     const int *lower;  // MFMA path: [K], 1 if prec_chol[k] has a non-zero below the diagonal
+    const float *prec_t;  // MFMA path: [K][d][d] prec_chol[k] transposed (k_transpose_sq)
 };
 
 __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
@@ -421,26 +422,33 @@ __global__ void __launch_bounds__(256, 2) k_community_async(CommArgs a) {
 }
 
 // GMM responsibilities on MFMA (d in {64, 128}): for each component the tile computes
-// Y = X P_k (A = the rows, lane (r, h) supplying x[row r][j = 2q + h] at k-step q; B = P_k staged
-// [j][c]: a half-wave reads 32 consecutive floats, conflict-free without padding), then
-// sum_c (Y - mu P_k)^2 per row: squares summed over the CT column tiles in registers, then over the
-// 32 columns of a half-wave with the DPP / permlane16 stages 0-4.  Per-component log-probabilities
-// go to resp_out itself (scratch, one row per lane group), the softmax over k finishes in place.
+// Y = X P_k (A = the rows, B = P_k), then sum_c (Y - mu P_k)^2 per row: squares summed over the CT
+// column tiles in registers, then over the 32 columns of a half-wave with the DPP / permlane16
+// stages 0-4.  Per-component log-probabilities go to resp_out itself (scratch, one row per lane
+// group), the softmax over k finishes in place.
+//
+// Operand layout: the k-steps pair feature indices s(g, i, h) = 8 g + 4 h + i (group g of four
+// k-steps), so a lane's four consecutive k-steps use four consecutive features: A comes from one
+// float4 of the row held in registers, B from one ds_read_b128 of P_k^T (rows = output columns c,
+// 4 consecutive s) -- one LDS instruction per 4 MFMAs per column tile instead of one per MFMA, and
+// group g + 1's B operands are read while group g's MFMAs run.  P^T (k_transpose_sq, once per
+// call) is staged into two half images (s < D/2, s >= D/2), rows padded to D/2 + 4 floats so the
+// 16 lanes of each b128 phase hit 16 distinct 4-bank groups.
 //
 // Triangular skip: sklearn's precisions_cholesky_ after an M-step is UPPER triangular
-// (solve_triangular(chol(cov), I, lower=True).T), so column tile ct only needs rows j <= 32 ct + 31
-// of P_k, i.e. k-steps q < 16 (ct + 1): 10 of the 16 32x32 blocks at d = 128 (0.625 of the MFMAs).
-// k_gmm_lower_flags marks the components with a non-zero below the diagonal (a lower factor, e.g.
-// sklearn's cholesky(precisions_init, lower=True)); those run the full loop.  The skipped MFMAs
-// would only add exact zeros, so both paths give identical results.
+// (solve_triangular(chol(cov), I, lower=True).T), so column tile ct only needs features s <= 32 ct
+// + 31 of P_k, i.e. groups g < 4 (ct + 1): 10 of the 16 32x32 blocks at d = 128 (0.625 of the
+// MFMAs).  k_gmm_lower_flags marks the components with a non-zero below the diagonal (a lower
+// factor, e.g. sklearn's cholesky(precisions_init, lower=True)); those run the full loop.  The
+// skipped MFMAs would only add exact zeros, so both paths give identical results.
 //
-// Staging is asynchronous: the k-steps q < S/2 read only rows j < D/2 of P_k ("half A"), the
-// others rows >= D/2 ("half B").  After every wavefront has finished half A of component k
-// (barrier), half A of P_{k+1} is copied global -> LDS by global_load_lds_dwordx4 (1 KiB per wave
-// instruction, lane-linear = the unpadded row-major image) while the half-B MFMAs and the epilogue
-// of k run; half B and mu_{k+1} P_{k+1} follow after the next barrier, in flight during the next
-// half A.  Each barrier is a plain __syncthreads (its vmcnt(0) retires exactly the copies the next
-// phase reads).  No VGPRs are spent on staging.
+// Staging is asynchronous: groups g < D/16 read only half image A, the others half image B.
+// After every wavefront has finished half A of component k (barrier), half A of P_{k+1}^T is copied
+// global -> LDS by global_load_lds_dwordx4 (1 KiB per wave instruction; each lane computes its own
+// source so the LDS image comes out padded) while the half-B MFMAs and the epilogue of k run; half
+// B and mu_{k+1} P_{k+1} follow after the next barrier, in flight during the next half A.  Each
+// barrier is a plain __syncthreads (its vmcnt(0) retires exactly the copies the next phase reads).
+// No VGPRs are spent on staging.
 __global__ void __launch_bounds__(256) k_gmm_lower_flags(const float *__restrict__ P, int D,
                                                          int *__restrict__ flags) {
     const float *Pk = P + (int64_t)blockIdx.x * D * D;
@@ -450,48 +458,94 @@ __global__ void __launch_bounds__(256) k_gmm_lower_flags(const float *__restrict
     if (threadIdx.x == 0) flags[blockIdx.x] = nz ? 1 : 0;
 }
 
-// One code path for both cases: the skippable MFMAs (a compile-time set after unrolling) are
-// guarded by the wave-uniform `full` flag; two unrolled copies pushed the kernel past 256 VGPRs.
-template <int D, int Q0, int Q1>
-__device__ __forceinline__ void resp_mfma_steps(
-    const float (&xa)[D / 2], const float *Ps, int h, int r, bool full,
-    __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
-    constexpr int CT = D / 32;
-#pragma unroll
-    for (int q = Q0; q < Q1; ++q) {
-        const float av = xa[q];
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-            if (q >= 16 * (ct + 1) && !full) continue;
-            const float bv = Ps[(2 * q + h) * D + ct * 32 + r];
-            acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ct], 0, 0, 0);
-        }
-    }
+// Pt[k][c][s] = P[k][s][c] (one D x D matrix per blockIdx.y, 32 x 32 tiles through LDS)
+__global__ void __launch_bounds__(256) k_transpose_sq(const float *__restrict__ P, int D,
+                                                      float *__restrict__ Pt) {
+    __shared__ float t[32][33];
+    const int tiles = D / 32;
+    const int tr = blockIdx.x / tiles, tc = blockIdx.x % tiles;
+    const float *src = P + (int64_t)blockIdx.y * D * D;
+    float *dst = Pt + (int64_t)blockIdx.y * D * D;
+    const int x = threadIdx.x & 31, y0 = threadIdx.x >> 5;
+    for (int y = y0; y < 32; y += 8) t[y][x] = src[(int64_t)(tr * 32 + y) * D + tc * 32 + x];
+    __syncthreads();
+    for (int y = y0; y < 32; y += 8) dst[(int64_t)(tc * 32 + y) * D + tr * 32 + x] = t[x][y];
 }
 
-// copy rows [half * D/2, half * D/2 + D/2) of P_k into the LDS image (wavefront wid of 4)
 template <int D>
-__device__ __forceinline__ void resp_stage_half(const float *Pk, float *sm, int half, int wid,
-                                                int lane) {
-    constexpr int PIECES = D * D / 2 / 256;  // 1 KiB wave instructions per half
+struct RespShape {
+    static constexpr int CT = D / 32;
+    static constexpr int G = D / 8;            // k-step groups
+    static constexpr int HLD = D / 2 + 4;      // padded row of a half image
+    static constexpr int HIMG = D * HLD;       // floats per half image
+    static constexpr int MP = 2 * HIMG;        // mu_k P_k (D floats, 256 reserved)
+    static constexpr int PARAMS = MP + 256;    // lower flag, log_norm (64 reserved)
+    static constexpr int LDS = PARAMS + 64;    // floats
+    static_assert(HIMG % 256 == 0, "a half image is a whole number of 1 KiB copies");
+};
+
+// groups [G0, G1) of one component: B operands of group g + 1 read while group g computes
+template <int D, int G0, int G1>
+__device__ __forceinline__ void resp_mfma_groups(
+    const __attribute__((ext_vector_type(4))) float (&xa)[D / 8], const float *sm, int h, int r,
+    bool full, __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
+    using RS = RespShape<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int CT = RS::CT;
+    auto fetch = [&](int g, f32x4 (&bv)[CT]) {
+        const float *img = sm + (g < RS::G / 2 ? 0 : RS::HIMG);
+        const int s0 = 8 * g - (g < RS::G / 2 ? 0 : D / 2) + 4 * h;
 #pragma unroll
-    for (int i = wid; i < PIECES; i += 4) {
-        const int off = half * (D * D / 2) + i * 256;
-        __builtin_amdgcn_global_load_lds(Pk + off + lane * 4, sm + off, 16, 0, 0);
+        for (int ct = 0; ct < CT; ++ct)
+            bv[ct] = *reinterpret_cast<const f32x4 *>(img + (ct * 32 + r) * RS::HLD + s0);
+    };
+    f32x4 bv[2][CT];
+    fetch(G0, bv[0]);
+#pragma unroll
+    for (int g = G0; g < G1; ++g) {
+        const int cur = (g - G0) & 1;
+        if (g + 1 < G1) fetch(g + 1, bv[cur ^ 1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                if (g >= 4 * (ct + 1) && !full) continue;
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[g][i], bv[cur][ct][i], acc[ct],
+                                                               0, 0, 0);
+            }
     }
 }
 
-// mu_k P_k (D floats) into sm[D*D .. D*D + 256): wavefront 0, lanes past D/4 re-read the last
+// copy half image `half` of P_k^T (rows c, features [half D/2, half D/2 + D/2), padded rows) into
+// LDS; wavefront wid of 4, 1 KiB per instruction; padding lanes re-read a valid address
+template <int D>
+__device__ __forceinline__ void resp_stage_half(const float *Ptk, float *sm, int half, int wid,
+                                                int lane) {
+    using RS = RespShape<D>;
+    constexpr int PIECES = RS::HIMG / 256;
+#pragma unroll
+    for (int j = 0; j < (PIECES + 3) / 4; ++j) {
+        const int i = wid + 4 * j;
+        if (i >= PIECES) break;  // wavefront-uniform
+        const int o = i * 256 + lane * 4;
+        const int c = o / RS::HLD, s = o % RS::HLD;
+        const int sc = s < D / 2 ? s : D / 2 - 4;
+        __builtin_amdgcn_global_load_lds(Ptk + c * D + half * (D / 2) + sc,
+                                         sm + half * RS::HIMG + i * 256, 16, 0, 0);
+    }
+}
+
+// mu_k P_k (D floats) into sm[MP .. MP + 256): wavefront 0, lanes past D/4 re-read the last
 // 16 B (their copies land in the unused tail of the 1 KiB region)
 template <int D>
 __device__ __forceinline__ void resp_stage_mp(const float *mp, float *sm, int wid, int lane) {
     if (wid == 0) {
         const int src = lane * 4 < D ? lane * 4 : D - 4;
-        __builtin_amdgcn_global_load_lds(mp + src, sm + D * D, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(mp + src, sm + RespShape<D>::MP, 16, 0, 0);
     }
 }
 
-// lower[k] and log_norm[k] into sm[D*D + 256 ..]: lanes 0 and 1 of wavefront 0 (a vector load of
+// lower[k] and log_norm[k] into sm[PARAMS ..]: lanes 0 and 1 of wavefront 0 (a vector load of
 // them would make the compiler wait vmcnt(0) at their first use -- draining the copies in flight;
 // loaded from LDS after the barrier instead)
 template <int D>
@@ -500,43 +554,47 @@ __device__ __forceinline__ void resp_stage_params(const RespArgs &a, int k, floa
     if (wid == 0) {
         const float *src = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
                                      : a.log_norm + k;
-        __builtin_amdgcn_global_load_lds(src, sm + D * D + 256, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(src, sm + RespShape<D>::PARAMS, 4, 0, 0);
     }
 }
 
 template <int D>
 __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
-    constexpr int S = D / 2;
-    constexpr int CT = D / 32;
+    using RS = RespShape<D>;
+    constexpr int CT = RS::CT;
+    constexpr int G = RS::G;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const float *Ps = sm;          // [D][D]
-    const float *mps = sm + D * D;  // [D] (+ tail up to 256), then 64 floats of params
+    const float *mps = sm + RS::MP;
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
     const int64_t blk0 = (int64_t)blockIdx.x * 128;
     const int64_t myrow = blk0 + wid * 32 + r;
     const bool rowok = myrow < a.V;
-    float xa[S];
+    f32x4 xa[G];  // xa[g][i] = x[row][8 g + 4 h + i]
 #pragma unroll
-    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + 2 * q + h] : 0.0f;
-    resp_stage_half<D>(a.prec_chol, sm, 0, wid, lane);
-    resp_stage_half<D>(a.prec_chol, sm, 1, wid, lane);
+    for (int g = 0; g < G; ++g) {
+        xa[g] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (rowok) xa[g] = *reinterpret_cast<const f32x4 *>(a.x + myrow * D + 8 * g + 4 * h);
+    }
+    resp_stage_half<D>(a.prec_t, sm, 0, wid, lane);
+    resp_stage_half<D>(a.prec_t, sm, 1, wid, lane);
     resp_stage_mp<D>(a.mu_prec, sm, wid, lane);
     resp_stage_params<D>(a, 0, sm, wid, lane);
     __syncthreads();
     for (int k = 0; k < a.K; ++k) {
-        const float *pr = sm + D * D + 256;
+        const float *pr = sm + RS::PARAMS;
         const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(pr[0])) != 0;
         const float lnk = pr[1];
-        const float *Pn = a.prec_chol + (int64_t)(k + 1) * D * D;
+        const float *Pn = a.prec_t + (int64_t)(k + 1) * D * D;
         f32x16 acc[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-        resp_mfma_steps<D, 0, S / 2>(xa, Ps, h, r, full, acc);
+        resp_mfma_groups<D, 0, G / 2>(xa, sm, h, r, full, acc);
         // the copies issued before the loop back-edge are not tracked by the compiler's barrier
         // fence (it emitted no vmcnt wait here): retire them explicitly before the barrier
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -545,7 +603,7 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
             resp_stage_half<D>(Pn, sm, 0, wid, lane);
             resp_stage_params<D>(a, k + 1, sm, wid, lane);
         }
-        resp_mfma_steps<D, S / 2, S>(xa, Ps, h, r, full, acc);
+        resp_mfma_groups<D, G / 2, G>(xa, sm, h, r, full, acc);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             float sq = 0.0f;
@@ -1295,8 +1353,16 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         rc = hip_error(hipGetLastError(), "k_gmm_lower_flags launch");
         if (rc) return rc;
         a.lower = flags;
+        float *pt = stream_scratch(dev, stream, kScratchGmmPt, sizeof(float) * (size_t)K * d * d);
+        if (!pt) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+        hipLaunchKernelGGL(k_transpose_sq, dim3((d / 32) * (d / 32), K), dim3(256), 0,
+                           (hipStream_t)stream, prec_chol, d, pt);
+        rc = hip_error(hipGetLastError(), "k_transpose_sq launch");
+        if (rc) return rc;
+        a.prec_t = pt;
         const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(d * d + 320);
+        const size_t lds = sizeof(float) * (size_t)(d == 64 ? RespShape<64>::LDS
+                                                             : RespShape<128>::LDS);
         void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_mfma<64> : k_gmm_resp_mfma<128>;
         static bool attr_m = false;
         if (!attr_m) {

@@ -27,7 +27,7 @@ int64_t *launch_counter(int device, void *stream);
 // Device scratch of at least `bytes` for launches on `stream` (library-owned, one buffer per
 // device, stream and slot, grows on demand: the first call at a larger size allocates, so capture
 // a stream only after a warm-up call of the same shape).
-constexpr int kScratchGmmFlags = 0, kScratchSlots = 1;
+constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchSlots = 2;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
 // One consistent snapshot of the process-wide launch options (come_set_option; mutex-guarded).
 // Every entry point takes it once at its start, or uses the caller's come_launch_opts (*_ex).
