@@ -8,7 +8,8 @@ Bars (written per test):
     bucket units of a sigmoid-table edge (OpenBLAS summation order can flip a bucket).
   * COME_MODE_HOGWILD (many walks in flight, races like the reference's threads): statistical --
     rows never touched stay bit-identical, per-row updates point where the sequential run's do
-    (cosine > 0.95) at low contention, bit-identical when walks share no row.
+    (cosine > 0.985 node / 0.965 ctx) at low contention, bit-identical when walks share no row;
+    held-out loss within 1% of the sequential oracle (tests/test_gpu_tierc.py).
   * community gradient / GMM responsibilities (fp32 contractions in a different summation
     order): rtol 1e-5 / atol 1e-5 vs the reference's numpy/sklearn outputs.
 """
@@ -39,10 +40,14 @@ def dev(a, dtype=None):
     return torch.from_numpy(a).to(DEV)
 
 
-def run_o2(node0, ctx0, walks, seeds, w, neg, table, lr, alpha, mode=tsi.MODE_SEQUENTIAL):
+def run_o2(node0, ctx0, walks, seeds, w, neg, table, lr, alpha, mode=tsi.MODE_SEQUENTIAL,
+           hot_share=None):
     node, ctx = dev(node0.copy()), dev(ctx0.copy())
+    tab = dev(table)
+    hot = None if hot_share is None else tsi.hot_rows(tab, node0.shape[0],
+                                                       max(1, int(hot_share * len(table))))
     tsi.sgns_o2(node, ctx, dev(walks.astype(np.int32)), dev(seeds.astype(np.uint64)), w, neg,
-                dev(table), lr, alpha, mode)
+                tab, lr, alpha, mode, hot=hot)
     torch.cuda.synchronize()
     return node.cpu().numpy(), ctx.cpu().numpy()
 
@@ -171,14 +176,17 @@ def test_o2_long_walk_truncated_at_max_sentence_len():
     np.testing.assert_array_equal(a[0], b[0])
 
 
-def test_o2_hogwild_statistics():
+@pytest.mark.parametrize("hot_share", [None, tsi.DEFAULT_HOT_P])
+def test_o2_hogwild_statistics(hot_share):
     """Many walks in flight, low row contention (the regime of the 1M-node benchmark): rows never
     touched stay bit-identical and the tables move as in the sequential (workers=1) run.  At
     lr=0.005 the updates are nearly order-independent (the oracle run in reversed walk order
     agrees with the forward run to cosine 0.998 on node rows, 0.99994 on context rows).  What
     is left is Hogwild itself: a row read-modify-written by two wavefronts at once keeps one
     update, and a store sits in one XCD's (non-coherent) L2 for microseconds before another XCD
-    sees it.  Measured on MI355X: cosine 0.992 (node) / 0.975 (ctx); bars 0.98 / 0.95."""
+    sees it.  Measured on MI355X (streaming kernel, 3 runs each, with and without the hot-row
+    bitmap): cosine 0.9911-0.9913 (node) / 0.9725-0.9729 (ctx), run-to-run spread < 5e-4; bars
+    0.985 / 0.965 (round 1: 0.98 / 0.95)."""
     rng = np.random.RandomState(5)
     V, d, L, P, w, neg = 500000, 128, 40, 1000, 5, 5
     table = orc.make_table(rng.randint(1, 50, V), 2000000)
@@ -186,7 +194,8 @@ def test_o2_hogwild_statistics():
     ctx0 = rng.uniform(-0.1, 0.1, (V, d)).astype(np.float32)
     walks = rng.randint(0, V // 2, (P, L)).astype(np.int32)  # rows >= V/2 never an input
     seeds = rng.randint(0, 2 ** 48, P, dtype=np.int64).astype(np.uint64)
-    hn, hc = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.005, 1.0, tsi.MODE_HOGWILD)
+    hn, hc = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.005, 1.0, tsi.MODE_HOGWILD,
+                    hot_share=hot_share)
     sn, sc = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.005, 1.0, tsi.MODE_SEQUENTIAL)
     np.testing.assert_array_equal(hn[V // 2:], node0[V // 2:])
     assert np.isfinite(hn).all() and np.isfinite(hc).all()
@@ -198,7 +207,7 @@ def test_o2_hogwild_statistics():
     cn = cos(hn[touched] - node0[touched], sn[touched] - node0[touched])
     cc = cos(hc - ctx0, sc - ctx0)
     print("hogwild vs sequential cosine: node %.5f ctx %.5f" % (cn, cc))
-    assert cn > 0.98 and cc > 0.95, (cn, cc)
+    assert cn > 0.985 and cc > 0.965, (cn, cc)
 
 
 def test_o2_hogwild_deterministic_when_walks_disjoint():
