@@ -41,13 +41,13 @@ def dev(a, dtype=None):
 
 
 def run_o2(node0, ctx0, walks, seeds, w, neg, table, lr, alpha, mode=tsi.MODE_SEQUENTIAL,
-           hot_share=None):
+           hot_share=None, opts=None):
     node, ctx = dev(node0.copy()), dev(ctx0.copy())
     tab = dev(table)
     hot = None if hot_share is None else tsi.hot_rows(tab, node0.shape[0],
                                                        max(1, int(hot_share * len(table))))
     tsi.sgns_o2(node, ctx, dev(walks.astype(np.int32)), dev(seeds.astype(np.uint64)), w, neg,
-                tab, lr, alpha, mode, hot=hot)
+                tab, lr, alpha, mode, hot=hot, opts=opts)
     torch.cuda.synchronize()
     return node.cpu().numpy(), ctx.cpu().numpy()
 
@@ -210,10 +210,11 @@ def test_o2_hogwild_statistics(hot_share):
     assert cn > 0.985 and cc > 0.965, (cn, cc)
 
 
-def test_o2_hogwild_deterministic_when_walks_disjoint():
+@pytest.mark.parametrize("kernel", [0, 1, 3])  # automatic (direct here), direct, streaming
+def test_o2_hogwild_deterministic_when_walks_disjoint(kernel):
     """Walks that share no row (inputs, positives) and draw no shared negative are independent:
-    Hogwild then equals the sequential run up to the rounding of its atomic write-back
-    (row += (cur - orig) instead of row = cur): <= 1e-6 abs."""
+    every Hogwild kernel then equals the sequential run bit for bit (same per-pair arithmetic,
+    plain stores for rows outside the hot bitmap)."""
     rng = np.random.RandomState(6)
     V, d, L, w, neg = 4096, 128, 16, 3, 0  # no negatives -> rows touched = the walk's own
     P = V // L
@@ -222,10 +223,11 @@ def test_o2_hogwild_deterministic_when_walks_disjoint():
     walks = rng.permutation(V).reshape(P, L).astype(np.int32)
     seeds = np.zeros(P, np.uint64)
     table = np.zeros(1, np.uint32)
-    a = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.05, 1.0, tsi.MODE_HOGWILD)
+    a = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.05, 1.0, tsi.MODE_HOGWILD,
+               opts={"o2_kernel": kernel})
     b = run_o2(node0, ctx0, walks, seeds, w, neg, table, 0.05, 1.0, tsi.MODE_SEQUENTIAL)
-    np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-6)
-    np.testing.assert_allclose(a[1], b[1], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
 
 
 def test_o2_dropin_per_walk_numpy_and_tensor():
