@@ -63,6 +63,38 @@ def cpu_port_baseline(walks_np, seeds_np, node_np, ctx_np, table_np, window, neg
     return pairs / el, pairs, done, el, int(orc.lib().oracle_mt_isa())
 
 
+def secondary_rows(timeout_s=240):
+    """The other hot-path rows measured on the same GPU after the timed region, each by
+    bench_aux.py in a child process (one JSON line each; CPU baselines skipped): C2 O1 pass,
+    C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass.  Outside the
+    timed region and never part of `value`; a failing row is reported as an error string."""
+    import subprocess
+    out = {}
+    for wl in ("c2", "c4", "walks"):
+        cmd = [sys.executable, os.path.join(ROOT, "bench_aux.py"), "--workload", wl,
+               "--steps", "10", "--warmup", "2", "--no-cpu-baseline"]
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or not line:
+                out[wl] = "error rc=%d: %s" % (r.returncode, r.stderr.strip()[-300:])
+                continue
+            j = json.loads(line[-1])
+            row = {"metric": j["metric"], "value": j["value"], "unit": j["unit"],
+                   "ms_per_step": j["ms_per_step"], "workload": j["config"]["workload"],
+                   "roofline_frac": j["roofline"]["frac"], "roofline_bound": j["roofline"]["bound"],
+                   "avg_kernel_ms": j["roofline"]["avg_kernel_ms"], "wall_s": time.time() - t0}
+            if wl == "c4":
+                for k in ("gmm_resp_ms", "gmm_resp_tflops_executed", "gmm_scatter_ms",
+                          "gmm_scatter_tflops_executed", "gmm_em_iteration_ms"):
+                    row[k] = j["config"][k]
+            out[wl] = row
+        except subprocess.TimeoutExpired:
+            out[wl] = "error: timed out after %ds" % timeout_s
+    return out
+
+
 def calibration_ratio():
     try:
         c = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))
@@ -136,6 +168,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this process may use (affinity and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N=1: skip the secondary rows (C2 / C4 / walker via bench_aux.py)")
     ap.add_argument("--sparse-sync", action="store_true",
                     help="N>1: exchange only the rows some rank changed (SparseDeltaAllReduce)")
     ap.add_argument("--measure-sync", action="store_true",
@@ -325,6 +359,11 @@ def main():
                              "AVX2+FMA" if isa else "baseline-ISA", threads, cw, cp, cel,
                              rthreads, "%.3f" % ratio if ratio else "n/a")}
 
+    secondary = None
+    if world == 1 and not args.no_secondary:
+        log("secondary rows (bench_aux.py c2 / c4 / walks, outside the timed region)")
+        secondary = secondary_rows()
+
     sync_measure = None
     if world == 1 and args.measure_sync:
         sync_measure = measure_sparse_sync(model, step, args.warmup, dev)
@@ -377,6 +416,8 @@ def main():
         },
         "cpu_baseline": cpu,
     }
+    if secondary is not None:
+        out["secondary"] = secondary
     if sync_measure is not None:
         out["sync_measure"] = sync_measure
     print(json.dumps(out), flush=True)

@@ -7,7 +7,7 @@ TAG=${TAG:-pmc}
 OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline ${BENCH_ARGS}"
+BENCH="$ROOT/bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline --no-secondary ${BENCH_ARGS}"
 i=0
 for C in "$@"; do
   i=$((i+1))

@@ -7,7 +7,7 @@ TAG=${TAG:-r01}
 OUT="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline ${BENCH_ARGS}"
+BENCH="$ROOT/bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-secondary ${BENCH_ARGS}"
 fatal() { [ "$1" -ne 0 ] && { echo "fatal rc=$1 in $2"; exit "$1"; }; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err"
 fatal $? trace
