@@ -178,8 +178,10 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: blocking delta all-reduce instead of overlapping it with the next "
                          "batch")
-    ap.add_argument("--packed-table", action="store_true",
-                    help="draw negatives from the exact packed table (come_pack_table)")
+    ap.add_argument("--plain-table", action="store_true",
+                    help="draw negatives from the reference's uint32 table instead of its exact "
+                         "packed form (come_pack_table; the product's default, Model."
+                         "negative_table)")
     ap.add_argument("--hot-p", type=float, default=None,
                     help="rows holding >= this share of the negative table are updated with "
                          "float atomics (default training_sdg_inner.DEFAULT_HOT_P; 0 = none)")
@@ -236,10 +238,11 @@ def main():
                       for s in range(total_steps)]
     sync_cls = SparseDeltaAllReduce if args.sparse_sync else DeltaAllReduce
     sync = sync_cls([model.node_embedding, model.context_embedding]) if world > 1 else None
-    # the reference's uint32 table, or its exact packed form (come_pack_table) with
-    # --packed-table (same draws; 1% slower at C3 on MI355X, profiles/r01_ab_dynamic_sched.txt)
-    neg_table = model.table_packed if args.packed_table and model.table_packed is not None \
-        else model.table
+    # the product's negative table (Model.negative_table): the exact packed form of the
+    # reference's uint32 table (same draws, 25 MB instead of 400 MB at T = 1e8), or with
+    # --plain-table the uint32 table itself
+    neg_table = model.table if args.plain_table else model.negative_table()
+    table_kind = "packed" if isinstance(neg_table, tsi.PackedTable) else "uint32"
 
     # target-row updates applied by the timed launches (the +-6 skip, pyx:141, leaves a target
     # row unwritten, so the bytes a launch must move depend on the data): counted in-kernel
@@ -329,6 +332,7 @@ def main():
             tj = json.load(open(args.traffic_json))
             if (tj.get("walks_per_launch") == B and tj.get("dim") == d
                     and tj.get("negative") == n and tj.get("lr") == args.lr
+                    and tj.get("negative_table", "uint32") == table_kind
                     and kernel_name(d, n).replace(" ", "") in
                     tj.get("kernel", "").replace(" ", "")):
                 traffic = tj.get("hbm_bytes_per_launch")
@@ -394,6 +398,7 @@ def main():
             "walks_per_step_per_gpu": B,
             "launch_opts": opts,
             "hot_rows": {"share_threshold": hot_p, "rows": n_hot},
+            "negative_table": table_kind,
             "pairs_per_step_per_gpu": pairs_rank_step,
             "sync_every_steps": args.sync_every if world > 1 else None,
             "parallelism": "walk-shard dp%d + %s delta all-reduce (%s)" % (

@@ -70,8 +70,10 @@ def c2(args):
     hot = m.hot_rows()  # the product's Hogwild launch (Node2Vec.train)
     n_hot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
 
+    table = m.table_packed if args.packed_table else m.table
+
     def step():
-        tsi.sgns_o1(m.node_embedding, edges, seeds[next(it) % len(seeds)], args.negative, m.table,
+        tsi.sgns_o1(m.node_embedding, edges, seeds[next(it) % len(seeds)], args.negative, table,
                     0.2, tsi.MODE_HOGWILD, hot=hot)
     el, ks = timed(step, args.steps, args.warmup)
     pairs = 2 * E
@@ -313,6 +315,8 @@ def main():
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--packed-table", action="store_true",
+                    help="c2: draw negatives from the exact packed table (come_pack_table)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="c4 with N > 1: nccl (= RCCL); gloo only to rehearse on one GPU")
     ap.add_argument("--all-ranks-device0", action="store_true",

@@ -145,6 +145,16 @@ struct Row {
         }
     }
 
+    // Non-temporal loads (global_load ... nt): rows with little reuse, so the L2 / Infinity Cache
+    // keep the small structures every wavefront reads (hot bitmap, packed negative table)
+    __device__ inline void load_nt(const float *__restrict__ row, int lane, int d) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const int e = lane + 64 * i;
+            v[i] = (FULL || e < d) ? __builtin_nontemporal_load(row + e) : 0.0f;
+        }
+    }
+
     // Agent-scope relaxed loads (global_load ... sc1): bypass this CU's L1, which other CUs'
     // stores never refresh (MI355X_MICROARCH.md: inter-workgroup visibility), so a row several
     // wavefronts update is read as last written to L2 / memory.
@@ -917,7 +927,11 @@ __global__ void __launch_bounds__(256)
         bool tnh[MAXN + 1];
         R in_n, pos_n, rn[MAXN + 1];
         int prev_i = -1;  // center of the pair just done
-        auto prefetch = [&](bool need_pos) {  // rows of the pair next_pair() just produced
+        // rows of the pair next_pair() just produced.  Negative rows are read non-temporally:
+        // random rows with little reuse, so the caches keep the packed negative table's words
+        // and the hot bitmap instead (with the packed table: 105.7-106.0 vs 108.1 ms per C3
+        // launch; no gain with the plain table, profiles/r03_ab_nt_sites.txt)
+        auto prefetch = [&](bool need_pos) {
             in_n.load(a.node + (int64_t)ncj * d, lane, d);
             if (need_pos) pos_n.load(a.ctx + (int64_t)nci * d, lane, d);
 #pragma unroll
@@ -926,7 +940,7 @@ __global__ void __launch_bounds__(256)
                 tn[k] = (int)(raw & ~kHotBit);
                 tnh[k] = (raw & kHotBit) != 0;
                 if (k > n) tn[k] = -1;
-                rn[k].load(a.ctx + (int64_t)(valid_row(tn[k]) ? tn[k] : 0) * d, lane, d);
+                rn[k].load_nt(a.ctx + (int64_t)(valid_row(tn[k]) ? tn[k] : 0) * d, lane, d);
             }
         };
         bool have = next_pair(nci, ncj, npi, nhi, nhj);

@@ -156,10 +156,12 @@ class Model(object):
         return cache[share]
 
     def negative_table(self):
-        """What the trainers pass to the kernels: the plain uint32 table, or its exact packed
-        form when ``use_packed_table`` is set (same draws; measured 1% slower at C3, where the
-        400 MB table's lines are not the bottleneck -- profiles/r01_ab_*.txt)."""
-        if getattr(self, "use_packed_table", False) and \
+        """What the trainers pass to the kernels: the exact packed form of the uint32 table
+        (come_pack_table: same draws, 16 B per 64 slots -- 25 MB instead of 400 MB at T = 1e8),
+        or the plain table when ``use_packed_table`` is False or the table did not pack.  With the
+        streaming O2 kernel's non-temporal negative-row loads the packed words stay cached:
+        105.7-106.0 vs 108.1 ms per C3 launch (profiles/r03_ab_nt_sites.txt)."""
+        if getattr(self, "use_packed_table", True) and \
                 getattr(self, "table_packed", None) is not None:
             return self.table_packed
         return self.table

@@ -44,6 +44,7 @@ def main(src, tag, kernel=KERNEL):
     ml = re.search(r"lr=([0-9.eE+-]+)", cfg["workload"])
     traffic = {"kernel": row["Name"], "tag": tag, "walks_per_launch": cfg["walks_per_step_per_gpu"],
                "dim": dim, "negative": neg, "lr": float(ml.group(1)) if ml else None,
+               "negative_table": cfg.get("negative_table", "uint32"),
                "hbm_bytes_per_launch": read_b + write_b,
                "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
                "algorithmic_bytes_per_launch": alg, "pairs_per_launch": pairs,

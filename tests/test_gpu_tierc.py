@@ -155,7 +155,7 @@ def c3_vocab_inputs(walks_n=131_072):
 
 def test_o2_hogwild_heldout_loss_at_benchmarked_shape():
     """Tier C at C3 itself: one bench launch (131,072 walks, 1.0e8 pair updates) of the product's
-    Hogwild path (streaming kernel) against the sequential oracle's held-out loss after the same
+    Hogwild path (streaming kernel, hot-row bitmap, packed negative table) against the sequential oracle's held-out loss after the same
     walks.  The oracle run takes ~3 minutes on one core, so its result is a committed fixture
     (tests/golden/tierc_c3_seq.json, scripts/make_tierc_fixture.py: the same inputs, sequential C
     oracle in walk order); the inputs' digest must match it.  Measured (profiles/
@@ -172,11 +172,13 @@ def test_o2_hogwild_heldout_loss_at_benchmarked_shape():
     assert abs(l0 - fx["init_loss"]) < 1e-9
     tab = dev(table)
     hot = tsi.hot_rows(tab, g.V, int(tsi.DEFAULT_HOT_P * len(table)))
+    packed = tsi.pack_table(tab)  # the product's negative table (Model.negative_table)
+    assert packed is not None
     l_hog = []
     for _ in range(2):
         node = dev(node0)
         ctx = torch.zeros_like(node)
-        tsi.sgns_o2(node, ctx, dev(train), dev(seeds), w, n, tab, lr, 1.0, tsi.MODE_HOGWILD,
+        tsi.sgns_o2(node, ctx, dev(train), dev(seeds), w, n, packed, lr, 1.0, tsi.MODE_HOGWILD,
                     hot=hot)
         torch.cuda.synchronize()
         l_hog.append(sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), rows_in, rows_pos,
