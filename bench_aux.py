@@ -8,8 +8,9 @@
                   (come_gmm_resp); each 2*V*K*d^2 flops; roofline = fp32 MFMA peak 157.3 TFLOP/s.
   --workload walks  SURVEY.md §8f row 1, the producer of C3's input: one corpus pass over the C3
                   graph (1M-node power law, every node starts one walk, length 80) on the HIP
-                  walker (come_random_walks); metric walk-steps/s; roofline HBM with 24 B per step
-                  (rowptr pair + one col entry + the written entry).  CPU baseline: the exact
+                  walker (come_random_walks); metric walk-steps/s; roofline: the measured 1.70
+                  random 128-B line reads per step against the Infinity-Cache random-gather rate
+                  (8.6 TB/s; 24 algorithmic B per step reported beside it).  CPU baseline: the exact
                   CPython-stream walker (come_walks_reference, native restatement of
                   graph_utils.build_deepwalk_corpus) on host threads.
 Each prints one JSON line.  CPU baselines: the reference's own code on a bounded sample
@@ -273,7 +274,13 @@ def walks(args):
     el, ks = timed(step, args.steps, args.warmup)
     steps_per_launch = float((out >= 0).sum().item() - g.V)  # moves (the start is not a step)
     avg = float(np.mean(ks)) / 1e3
-    bps = 24
+    bps = 24  # algorithmic: rowptr pair + one col entry + the written entry
+    # What bounds it: each step is a dependent chain of random 128-B line reads -- 1.70 requests
+    # per step measured (profiles/r03_pmc_walks.json: rowptr line, col line, 17% L2 hits), served
+    # by the Infinity Cache (rowptr + col = 88 MB at C3) -> priced against the guide's
+    # Infinity-Cache random-gather rate
+    req_bytes = 1.70 * 128
+    ic_peak = 8600.0  # GB/s, MI355X_MICROARCH.md 'Indexed rows': 38 MB table, random rows (IC)
     cpu = None
     if not args.no_cpu_baseline:
         Gh = gu.Graph(np.arange(1, g.V + 1), g.rowptr, g.col.astype(np.int32), g.degree,
@@ -296,10 +303,14 @@ def walks(args):
         "higher_is_better": True, "dtype": "int32", "data": "synthetic Chung-Lu (seed 1)",
         "config": {"workload": "walk corpus pass: V=%d, E=%d, L=%d, alpha=0" % (
             g.V, g.num_edges, L)},
-        "roofline": {"bound": "hbm", "achieved": bps * steps_per_launch / avg / 1e9,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": bps * steps_per_launch / avg / 1e9 / HBM_PEAK_GBS,
-                     "bytes_per_step": bps, "avg_kernel_ms": avg * 1e3},
+        "roofline": {"bound": "infinity-cache gathers",
+                     "achieved": req_bytes * steps_per_launch / avg / 1e9,
+                     "peak": ic_peak, "unit": "GB/s",
+                     "frac": req_bytes * steps_per_launch / avg / 1e9 / ic_peak,
+                     "request_bytes_per_step": req_bytes,
+                     "algorithmic_bytes_per_step": bps,
+                     "algorithmic_frac_of_hbm": bps * steps_per_launch / avg / 1e9 / HBM_PEAK_GBS,
+                     "avg_kernel_ms": avg * 1e3},
         "cpu_baseline": cpu}))
 
 
