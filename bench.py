@@ -2,7 +2,8 @@
 configs[2] = SURVEY.md §8d C3), 1..8 MI355X, walk shard + periodic RCCL delta all-reduce.
 
 One "step" = one O2 launch (come_sgns_o2, Hogwild, one wavefront per walk) over a batch of
-`--walks-per-step` random walks already resident in HBM, plus -- for N > 1, every `--sync-every`
+`--walks-per-step` random walks already resident in HBM (default 1,048,576 = one corpus pass of the
+1M-node graph = the product's launch, Context2Vec.batch_walks), plus -- for N > 1, every `--sync-every`
 steps -- the delta all-reduce of both embedding tables over RCCL.  Every rank trains its own walk
 shard (weak scaling).  Printed by rank 0: ONE JSON line (contract in the task statement), with
 `roofline` (dominant kernel: achieved algorithmic HBM bytes / launch time vs the 8 TB/s peak) and,
@@ -160,7 +161,11 @@ def main():
     ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--walk-length", type=int, default=80)
-    ap.add_argument("--walks-per-step", type=int, default=1 << 17)
+    # one step = one product launch: Context2Vec.batch_walks (1 << 20) walks, i.e. one C3 corpus
+    # pass (every node starts one walk).  Walks in flight are bounded by the resident wavefronts
+    # (8,192), not by the batch; a smaller batch only adds launch tails (ms per 1e8 pairs at
+    # 65k / 131k / 262k walks per launch: 106.3 / 104.8 / 102.1, profiles/r03_ab_batch.txt)
+    ap.add_argument("--walks-per-step", type=int, default=1 << 20)
     ap.add_argument("--table-size", type=int, default=100_000_000)
     ap.add_argument("--lr", type=float, default=0.1)  # lr 0.1, alpha 1
     ap.add_argument("--sync-every", type=int, default=1)
@@ -342,7 +347,7 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as orc
-        sample = min(2 * B, walks_all.shape[0])  # more than --cpu-seconds can finish
+        sample = min(400_000, walks_all.shape[0])  # more than --cpu-seconds can finish
         wn = walks_all[:sample].cpu().numpy()
         sn = seeds_all[:sample].cpu().numpy().view(np.uint64)
         node_h = np.ascontiguousarray(model.node_embedding.cpu().numpy())

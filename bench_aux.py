@@ -71,7 +71,7 @@ def c2(args):
     hot = m.hot_rows()  # the product's Hogwild launch (Node2Vec.train)
     n_hot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
 
-    table = m.table_packed if args.packed_table else m.table
+    table = m.table if args.plain_table else m.negative_table()  # the product's (packed) table
 
     def step():
         tsi.sgns_o1(m.node_embedding, edges, seeds[next(it) % len(seeds)], args.negative, table,
@@ -115,7 +115,8 @@ def c2(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True, "dtype": "f32", "data": "synthetic SBM (seed 0)",
         "config": {"workload": "configs[1]/C2: O1 over %d edges of a 100x1000 SBM, d=%d, "
-                               "negative=%d, lr=0.2" % (E, d, n), "hot_rows": n_hot},
+                               "negative=%d, lr=0.2" % (E, d, n), "hot_rows": n_hot,
+                   "negative_table": "uint32" if args.plain_table else "packed"},
         "roofline": {"bound": "hbm", "achieved": bpp * pairs / avg / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": bpp * pairs / avg / 1e9 / HBM_PEAK_GBS,
                      "bytes_per_pair": bpp, "avg_kernel_ms": avg * 1e3},
@@ -326,8 +327,9 @@ def main():
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--packed-table", action="store_true",
-                    help="c2: draw negatives from the exact packed table (come_pack_table)")
+    ap.add_argument("--plain-table", action="store_true",
+                    help="c2: draw negatives from the uint32 table instead of the product's "
+                         "exact packed form (Model.negative_table)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="c4 with N > 1: nccl (= RCCL); gloo only to rehearse on one GPU")
     ap.add_argument("--all-ranks-device0", action="store_true",
