@@ -154,7 +154,8 @@ def c3_vocab_inputs(walks_n=131_072):
 
 
 def test_o2_hogwild_heldout_loss_at_benchmarked_shape():
-    """Tier C at C3 itself: one bench launch (131,072 walks, 1.0e8 pair updates) of the product's
+    """Tier C at C3 itself: one launch (131,072 walks, 1.0e8 pair updates; the bench and the
+    product launch 1,048,576 walks of the same kernel at the same concurrency) of the product's
     Hogwild path (streaming kernel, hot-row bitmap, packed negative table) against the sequential oracle's held-out loss after the same
     walks.  The oracle run takes ~3 minutes on one core, so its result is a committed fixture
     (tests/golden/tierc_c3_seq.json, scripts/make_tierc_fixture.py: the same inputs, sequential C
