@@ -604,21 +604,45 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
             resp_stage_params<D>(a, k + 1, sm, wid, lane);
         }
         resp_mfma_groups<D, G / 2, G>(xa, sm, h, r, full, acc);
+        float sq[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            float sq = 0.0f;
+            sq[e] = 0.0f;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 const float y = acc[ct][e] - mps[ct * 32 + r];
-                sq = __builtin_fmaf(y, y, sq);
+                sq[e] = __builtin_fmaf(y, y, sq[e]);
             }
-            sq = reduce_stage<0>(sq);
-            sq = reduce_stage<1>(sq);
-            sq = reduce_stage<2>(sq);
-            sq = reduce_stage<3>(sq);
-            sq = reduce_stage<4>(sq);
+        }
+        // Sum over the 32 columns r of a half-wave for each of its 16 rows e: a reduce-scatter
+        // butterfly (each stage keeps half of the values and adds the partner's copy of them), so
+        // lane r ends with row e(r) = 8 b3 + 4 b2 + 2 b0 + b1 (b = bits of r) after 8+4+2+1 DPP
+        // adds + one permlane16 add, and the wave stores all 32 rows of the tile at once.  The
+        // partners are mirrors first (they flip the lower bits too, so they must come before
+        // the quad stages): row_mirror (bit 3), row_half_mirror (bit 2), then quad xor 1 and 2.
+        const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
+        auto scatter_stage = [](float *v, int n, int keep_hi, auto partner) {
+#pragma unroll
+            for (int i = 0; i < n; ++i) {
+                const float keep = keep_hi ? v[i + n] : v[i];
+                const float send = keep_hi ? v[i] : v[i + n];
+                v[i] = keep + partner(send);
+            }
+        };
+        auto dpp = [](float x, auto ctrl) {
+            return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
+                                                              decltype(ctrl)::value, 0xF, 0xF,
+                                                              false));
+        };
+        scatter_stage(sq, 8, b3, [&](float x) { return dpp(x, std::integral_constant<int, 0x140>{}); });
+        scatter_stage(sq, 4, b2, [&](float x) { return dpp(x, std::integral_constant<int, 0x141>{}); });
+        scatter_stage(sq, 2, b0, [&](float x) { return dpp(x, std::integral_constant<int, 0xB1>{}); });
+        scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
+        const float tot = reduce_stage<4>(sq[0]);  // + the other 16 columns (lane r ^ 16)
+        {
+            const int e = 8 * b3 + 4 * b2 + 2 * b0 + b1;
             const int64_t row = blk0 + wid * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            if (r == 0 && row < a.V) a.resp[row * a.K + k] = lnk - 0.5f * sq;
+            if (r < 16 && row < a.V) a.resp[row * a.K + k] = lnk - 0.5f * tot;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // half B of P_k and mu_k P_k free; half A of P_{k+1} in LDS
