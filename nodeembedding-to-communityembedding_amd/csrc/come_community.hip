@@ -584,6 +584,10 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
     resp_stage_mp<D>(a.mu_prec, sm, wid, lane);
     resp_stage_params<D>(a, 0, sm, wid, lane);
     __syncthreads();
+    // the row this lane's reduce-scatter ends on (lanes r < 16 of each half-wave; see below)
+    const int my_e = 8 * ((r >> 3) & 1) + 4 * ((r >> 2) & 1) + 2 * (r & 1) + ((r >> 1) & 1);
+    const int64_t my_row = blk0 + wid * 32 + (my_e & 3) + 8 * (my_e >> 2) + 4 * h;
+    float run_max = -INFINITY, run_sum = 0.0f;
     for (int k = 0; k < a.K; ++k) {
         const float *pr = sm + RS::PARAMS;
         const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(pr[0])) != 0;
@@ -640,9 +644,15 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
         scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
         const float tot = reduce_stage<4>(sq[0]);  // + the other 16 columns (lane r ^ 16)
         {
-            const int e = 8 * b3 + 4 * b2 + 2 * b0 + b1;
-            const int64_t row = blk0 + wid * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            if (r < 16 && row < a.V) a.resp[row * a.K + k] = lnk - 0.5f * tot;
+            const float lp = lnk - 0.5f * tot;
+            if (r < 16 && my_row < a.V) a.resp[my_row * a.K + k] = lp;
+            // online log-sum-exp of the row's components so far
+            if (lp > run_max) {
+                run_sum = run_sum * expf(run_max - lp) + 1.0f;
+                run_max = lp;
+            } else {
+                run_sum += expf(lp - run_max);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // half B of P_k and mu_k P_k free; half A of P_{k+1} in LDS
@@ -651,17 +661,13 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
             resp_stage_mp<D>(a.mu_prec + (int64_t)(k + 1) * D, sm, wid, lane);
         }
     }
-    __threadfence_block();
-    __syncthreads();
-    if (tid < 128 && blk0 + tid < a.V) {
-        float *lp = a.resp + (blk0 + tid) * a.K;
-        float m = -INFINITY;
-        for (int k = 0; k < a.K; ++k) m = fmaxf(m, lp[k]);
-        float s = 0.0f;
-        for (int k = 0; k < a.K; ++k) s += expf(lp[k] - m);
-        const float lse = m + logf(s);
+    // softmax over k in place: the lane that wrote the row's log-probabilities normalises them
+    // (one read-write pass; max and sum were kept online)
+    if (r < 16 && my_row < a.V) {
+        float *lp = a.resp + my_row * a.K;
+        const float lse = run_max + logf(run_sum);
         for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
-        if (a.lse) a.lse[blk0 + tid] = lse;
+        if (a.lse) a.lse[my_row] = lse;
     }
 }
 
