@@ -64,7 +64,7 @@ def cpu_port_baseline(walks_np, seeds_np, node_np, ctx_np, table_np, window, neg
     return pairs / el, pairs, done, el, int(orc.lib().oracle_mt_isa())
 
 
-def secondary_rows(timeout_s=240):
+def secondary_rows(timeout_s=150):
     """The other hot-path rows measured on the same GPU after the timed region, each by
     bench_aux.py in a child process (one JSON line each; CPU baselines skipped): C2 O1 pass,
     C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass.  Outside the
