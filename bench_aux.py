@@ -68,7 +68,7 @@ def c2(args):
              for _ in range(args.steps + args.warmup)]
     it = iter(range(10 ** 9))
 
-    hot = m.hot_rows()  # the product's Hogwild launch (Node2Vec.train)
+    hot = m.hot_rows(args.hot_p)  # the product's Hogwild launch (Node2Vec.train)
     n_hot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
 
     table = m.table if args.plain_table else m.negative_table()  # the product's (packed) table
@@ -327,6 +327,9 @@ def main():
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hot-p", type=float, default=None,
+                    help="c2: contended-row share (default training_sdg_inner.DEFAULT_HOT_P; "
+                         "0 = no float-atomic rows)")
     ap.add_argument("--plain-table", action="store_true",
                     help="c2: draw negatives from the uint32 table instead of the product's "
                          "exact packed form (Model.negative_table)")
