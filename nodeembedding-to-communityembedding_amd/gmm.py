@@ -86,6 +86,20 @@ def resp_t_x(resp, X, chunks=256):
     return part
 
 
+def resp_sum(resp, chunks=256):
+    """[K] float64: resp.sum(0) as fp32 sums over `chunks` row blocks added in float64 (0.06 vs
+    0.27 ms for a float64-accumulating column sum at C4)."""
+    import torch
+    V, K = resp.shape
+    n = V // chunks * chunks
+    if n == 0:
+        return resp.sum(0, dtype=torch.float64)
+    part = resp[:n].reshape(chunks, n // chunks, K).sum(1).double().sum(0)
+    if n < V:
+        part = part + resp[n:].sum(0, dtype=torch.float64)
+    return part
+
+
 def scatter(X, resp, means, chunks=None):
     """[K, d, d] device fp32: sum_i resp[i,k] (x_i - means_k)(x_i - means_k)^T."""
     import torch
@@ -153,7 +167,7 @@ class GaussianMixture(object):
         import torch
         V, d = X.shape
         world = self._rank_world()[1]
-        nk = resp.sum(0, dtype=torch.float64)
+        nk = resp_sum(resp)
         sx = resp_t_x(resp, X)
         if world > 1:
             all_reduce_sum([nk, sx], self.group)

@@ -31,7 +31,7 @@ def main():
         ev[0].record()
         resp, _ = gmm.estep(X, gm._e_pc, gm._e_mp, gm._e_ln)
         ev[1].record()
-        nk = resp.sum(0, dtype=torch.float64)
+        nk = gmm.resp_sum(resp)
         sx = gmm.resp_t_x(resp, X)
         nk = nk + 1e-15
         means = sx / nk[:, None]

@@ -32,3 +32,18 @@ for C in (64, 256, 1000, 4000):
 ms, o = t(lambda: splitk64(1000))
 print("splitk64 1000", round(ms, 3))
 r64 = resp.double(); X64 = X.double()
+# k-means centre sums: index_add_ of V rows into K rows vs a one-hot split-K batched GEMM
+labels = torch.randint(0, K, (V,), device=dev)
+def ia():
+    S = torch.zeros((K, d), dtype=torch.float32, device=dev)
+    S.index_add_(0, labels, X)
+    return S
+def oh():
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from come_amd import gmm
+    return gmm.resp_t_x(torch.nn.functional.one_hot(labels, K).float(), X).float()
+ms_ia, s_ia = t(ia)
+ms_oh, s_oh = t(oh)
+print("index_add_", round(ms_ia, 3), "one-hot split-K", round(ms_oh, 3),
+      float((s_ia - s_oh).abs().max() / s_ia.abs().max()))
