@@ -203,3 +203,21 @@ def test_community_train_unknown_node_raises_keyerror():
     cm.lr, cm.distributed, cm.group = 0.1, False, None
     with pytest.raises(KeyError):
         cm.train([1, 2, 999], m, 0.01)
+
+
+@pytest.mark.parametrize("V,K,d", [(1000, 7, 5), (100, 3, 4), (256 * 3 + 17, 50, 9), (256, 2, 3)])
+def test_gmm_split_k_sums_equal_float64_reference(V, K, d):
+    """gmm.resp_t_x / resp_sum (the M-step's means numerator and nk as chunked sums added in
+    float64, gmm.py) equal the float64 products within fp32 partial-sum error, for V not a
+    multiple of the chunk count and V below it."""
+    import torch
+    from come_amd import gmm
+    rng = np.random.RandomState(V + K)
+    resp = torch.from_numpy(rng.dirichlet(np.ones(K), V).astype(np.float32))
+    X = torch.from_numpy(rng.normal(size=(V, d)).astype(np.float32))
+    ref_sx = resp.double().t() @ X.double()
+    ref_nk = resp.double().sum(0)
+    sx, nk = gmm.resp_t_x(resp, X), gmm.resp_sum(resp)
+    assert sx.dtype == torch.float64 and nk.dtype == torch.float64
+    np.testing.assert_allclose(sx.numpy(), ref_sx.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(nk.numpy(), ref_nk.numpy(), rtol=1e-6, atol=1e-6)
