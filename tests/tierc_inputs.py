@@ -1,0 +1,103 @@
+"""Tier-C inputs and the held-out loss (TEST INFRASTRUCTURE; SURVEY.md §8c tier C).
+
+Inputs that are built on the host only -- Chung-Lu graph, the reference's make_table, walks from the
+exact CPython-stream host walker (graph_utils._corpus, utils/graph_utils.py:20-46 + 187-192),
+numpy RandomState picks / initial tables / per-walk seeds -- so the sequential oracle can replay
+them anywhere (in the container, for a committed fixture) and the GPU side rebuilds the same
+arrays on the box; the two are matched by a digest of the inputs.
+
+No torch here: the fixture scripts run on a CPU-only host.
+"""
+import hashlib
+import random
+
+import numpy as np
+
+
+def log_sigmoid(x):
+    return -np.logaddexp(0.0, -x)
+
+
+def sgns_loss(inp, out, rows_in, rows_pos, rows_neg, chunk=20000):
+    """Mean held-out SGNS loss (float64, exact sigmoid): -log s(u.c+) - sum_k log s(-u.c_k),
+    over pairs (rows_in[p], rows_pos[p], rows_neg[p, :]), evaluated `chunk` pairs at a time."""
+    total = 0.0
+    m = len(rows_in)
+    for s in range(0, m, chunk):
+        ri, rp, rn = rows_in[s:s + chunk], rows_pos[s:s + chunk], rows_neg[s:s + chunk]
+        u = inp[ri].astype(np.float64)
+        lp = log_sigmoid(np.einsum("pd,pd->p", u, out[rp].astype(np.float64)))
+        ln = log_sigmoid(-np.einsum("pd,pkd->pk", u, out[rn].astype(np.float64))).sum(1)
+        total += float((lp + ln).sum())
+    return -total / m
+
+
+def heldout_o2_pairs(walks, w, n, table, count, seed):
+    """`count` (input row, positive row) window pairs of held-out walks (pyx:494-506: input
+    idx[j], positive idx[i]) with n negatives each drawn from the negative table."""
+    rng = np.random.RandomState(seed)
+    P, L = walks.shape
+    p = rng.randint(0, P, 4 * count)
+    i = rng.randint(0, L, 4 * count)
+    off = rng.randint(1, w + 1, 4 * count) * rng.choice([-1, 1], 4 * count)
+    j = i + off
+    ok = (j >= 0) & (j < L)
+    p, i, j = p[ok], i[ok], j[ok]
+    ci, cj = walks[p, i], walks[p, np.clip(j, 0, L - 1)]
+    ok = (ci >= 0) & (cj >= 0)
+    ci, cj = ci[ok][:count], cj[ok][:count]
+    neg = table[rng.randint(0, len(table), (len(ci), n))].astype(np.int64)
+    return cj, ci, neg
+
+
+class HostInputs(object):
+    """One tier-C workload built on the host (see the module docstring)."""
+
+    def __init__(self, V, graph_seed, d, train_walks, held_walks=20000, T=100_000_000,
+                 walk_streams=(11, 12), pick_seed=7, L=80, mean_degree=20.0):
+        from oracle import oracle as orc
+        from come_amd import graph_utils as gu
+        from come_amd.graph import chung_lu
+        g = chung_lu(V, mean_degree, gamma=2.5, seed=graph_seed)
+        self.g = g
+        self.table = orc.make_table(g.degree.astype(np.float64), T)
+        gh = gu.Graph(np.arange(1, g.V + 1), g.rowptr, g.col.astype(np.int32), g.degree,
+                      np.zeros((0, 2), np.int32))
+        walks = gu._corpus(gh, [1] * len(walk_streams), L, 0.0,
+                           [random.Random(s) for s in walk_streams], threads=len(walk_streams))
+        walks = np.asarray(walks, np.int32)
+        rng = np.random.RandomState(pick_seed)
+        pick = rng.choice(walks.shape[0], train_walks + held_walks, replace=False)
+        walks = walks[pick]
+        self.train, self.held = walks[:train_walks], walks[train_walks:]
+        self.node0 = rng.uniform(-1, 1, (g.V, d)).astype(np.float32)
+        self.seeds = rng.randint(0, 2 ** 48, train_walks, dtype=np.int64).astype(np.uint64)
+        self.digest = hashlib.sha256(walks.tobytes() + self.seeds.tobytes() +
+                                     self.node0.tobytes()[:1 << 20] +
+                                     self.table.tobytes()[:1 << 20]).hexdigest()
+
+    def heldout(self, w, n, count=200_000, seed=24):
+        return heldout_o2_pairs(self.held, w, n, self.table, count, seed)
+
+
+# configs[4]/C5's kernel (d = 256, n = 10) on a graph the single-core oracle can
+# replay: Chung-Lu 1M nodes (C5's generator and seed, 1/10 of its nodes), T = 1e8, one launch of
+# 131,072 walks (1.0e8 pair updates), lr 0.1, w 5, L 80.
+C5 = dict(V=1_000_000, graph_seed=4, d=256, train_walks=131_072, walk_streams=(41,),
+          pick_seed=43)
+C5_HYPER = dict(window=5, negative=10, lr=0.1)
+
+
+def c5_inputs():
+    return HostInputs(**C5)
+
+
+# configs[2]/C3 at the bench's own launch: the 1M-node graph, one launch of 1,048,576 walks
+# (8.07e8 pair updates); fixture tests/golden/tierc_c3_1m_seq.json (scripts/tierc_c3_1m.py).
+C3_1M = dict(V=1_000_000, graph_seed=1, d=128, train_walks=1 << 20, walk_streams=(11, 12),
+             pick_seed=7)
+C3_HYPER = dict(window=5, negative=5, lr=0.1)
+
+
+def c3_1m_inputs():
+    return HostInputs(**C3_1M)
