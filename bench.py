@@ -1,11 +1,13 @@
 """Benchmark: SGNS pair-updates/sec at d=128 on a 1M-node power-law graph (BASELINE.json metric,
 configs[2] = SURVEY.md §8d C3), 1..8 MI355X, walk shard + periodic RCCL delta all-reduce.
 
-One "step" = one O2 launch (come_sgns_o2, Hogwild, one wavefront per walk) over a batch of
-`--walks-per-step` random walks already resident in HBM (default 1,048,576 = one corpus pass of the
-1M-node graph = the product's launch, Context2Vec.batch_walks), plus -- for N > 1, every `--sync-every`
-steps -- the delta all-reduce of both embedding tables over RCCL.  Every rank trains its own walk
-shard (weak scaling).  Printed by rank 0: ONE JSON line (contract in the task statement), with
+One "step" = the product trainer (Context2Vec.train_rows) over a batch of `--walks-per-step`
+random walks per rank already resident in HBM (default 1,048,576 = one corpus pass of the 1M-node
+graph = the product's launch, Context2Vec.batch_walks): at N = 1 one O2 launch (come_sgns_o2,
+Hogwild, one wavefront per walk); at N > 1 one launch per `--sync-walks` of the rank's walks, each
+followed by the delta all-reduce of both embedding tables over RCCL (overlapped with the next
+launch; the step's last exchange blocking).  The ranks train contiguous shards of ONE corpus
+(weak scaling: per-rank work fixed).  Printed by rank 0: ONE JSON line (contract in the task statement), with
 `roofline` (dominant kernel: achieved algorithmic HBM bytes / launch time vs the 8 TB/s peak) and,
 at N = 1, `cpu_baseline` (the builder's Hogwild C restatement of the reference's CPU path, timed on
 every core this process may use; its ratio to the reference's own Cython is calibrated in the
@@ -168,7 +170,9 @@ def main():
     ap.add_argument("--walks-per-step", type=int, default=1 << 20)
     ap.add_argument("--table-size", type=int, default=100_000_000)
     ap.add_argument("--lr", type=float, default=0.1)  # lr 0.1, alpha 1
-    ap.add_argument("--sync-every", type=int, default=1)
+    ap.add_argument("--sync-walks", type=int, default=None,
+                    help="N>1: walks each rank trains between two delta exchanges (default "
+                         "context_embeddings.DEFAULT_SYNC_WALKS)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this process may use (affinity and cgroup quota)")
@@ -203,7 +207,7 @@ def main():
     import torch.distributed as dist
 
     import come_amd.training_sdg_inner as tsi
-    from come_amd.distributed import DeltaAllReduce, SparseDeltaAllReduce
+    from come_amd.context_embeddings import DEFAULT_SYNC_WALKS, Context2Vec
     from come_amd.graph import chung_lu, random_walks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -221,7 +225,10 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    # ---- workload: C3 (same graph on every rank; walks sharded by rank) ----
+    # ---- workload: C3.  Same graph on every rank; ONE corpus of world x (warmup + steps) x B
+    # walks (every pass a fresh permutation of the start nodes, graph_utils.py:187-192) with one
+    # seed per walk, sharded contiguously over the ranks: rank r generates exactly its shard's
+    # walks (the walker's Philox counter is the walk's global index) ----
     t0 = time.time()
     g = chung_lu(args.nodes, args.mean_degree, gamma=2.5, seed=1)
     V, d, n, w, L = g.V, args.dim, args.negative, args.window, args.walk_length
@@ -233,74 +240,67 @@ def main():
             V, g.num_edges, time.time() - t0, V * d * 4 / 1e6, args.table_size * 4 / 1e6))
     B = args.walks_per_step
     total_steps = args.warmup + args.steps
-    passes = (total_steps * B + V - 1) // V
-    walks_all = random_walks(g, passes, L, seed=100 + rank, device=dev)[:total_steps * B]
-    walks_all = walks_all.contiguous()
-    np.random.seed(5678 + rank)
-    seeds_all = torch.from_numpy(tsi.draw_seeds(total_steps * B).view(np.int64)).to(dev)
+    per_rank = total_steps * B
+    lo = rank * per_rank
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(100)
+    passes = (world * per_rank + V - 1) // V
+    starts = torch.cat([torch.randperm(V, generator=gen, device=dev) for _ in range(passes)])
+    walks_all = random_walks(g, 0, L, seed=100, device=dev,
+                             starts=starts[lo:lo + per_rank], walk_offset=lo).contiguous()
+    del starts
+    gen.manual_seed(5678)
+    seeds_all = torch.randint(0, 2 ** 48, (world * per_rank,), generator=gen, device=dev,
+                              dtype=torch.int64)[lo:lo + per_rank].contiguous()
     lengths = (walks_all >= 0).sum(dim=1)
     pairs_per_step = [int(o2_pairs_of_lengths(lengths[s * B:(s + 1) * B], w))
                       for s in range(total_steps)]
-    sync_cls = SparseDeltaAllReduce if args.sparse_sync else DeltaAllReduce
-    sync = sync_cls([model.node_embedding, model.context_embedding]) if world > 1 else None
-    # the product's negative table (Model.negative_table): the exact packed form of the
-    # reference's uint32 table (same draws, 25 MB instead of 400 MB at T = 1e8), or with
-    # --plain-table the uint32 table itself
-    neg_table = model.table if args.plain_table else model.negative_table()
+    sync_walks = args.sync_walks or DEFAULT_SYNC_WALKS
+    # the product's trainer (Context2Vec.train_rows = what Context2Vec.train runs after mapping
+    # the corpus): one launch per batch_walks at N = 1; at N > 1 one launch per sync_walks of
+    # the rank's shard, each followed by the delta exchange (overlapped with the next launch, the
+    # last one blocking)
+    opts = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)} or None
+    hot_p = tsi.DEFAULT_HOT_P if args.hot_p is None else args.hot_p
+    learner = Context2Vec(lr=args.lr, window_size=w, negative=n, batch_walks=B,
+                          distributed=world > 1, sync_walks=sync_walks,
+                          sparse_sync=args.sparse_sync, overlap=not args.no_overlap,
+                          hot_share=hot_p, launch_opts=opts)
+    if args.plain_table:
+        model.use_packed_table = False
+    neg_table = model.negative_table()
     table_kind = "packed" if isinstance(neg_table, tsi.PackedTable) else "uint32"
 
     # target-row updates applied by the timed launches (the +-6 skip, pyx:141, leaves a target
     # row unwritten, so the bytes a launch must move depend on the data): counted in-kernel
     upd_count = torch.zeros(1, dtype=torch.int64, device=dev)
-    opts = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)} or None
-    hot_p = tsi.DEFAULT_HOT_P if args.hot_p is None else args.hot_p
     hot = model.hot_rows(hot_p)
     n_hot = 0 if hot is None else int(np.unpackbits(hot.cpu().numpy().view(np.uint8)).sum())
 
-    def step(s, count=False):
-        tsi.sgns_o2(model.node_embedding, model.context_embedding, walks_all[s * B:(s + 1) * B],
-                    seeds_all[s * B:(s + 1) * B], w, n, neg_table, args.lr, 1.0,
-                    tsi.MODE_HOGWILD, opts=opts, update_count=upd_count if count else None,
-                    hot=hot)
+    def step(s, count=False, events=None):
+        learner.train_rows(model, walks_all[s * B:(s + 1) * B], seeds_all[s * B:(s + 1) * B],
+                           1.0, update_count=upd_count if count else None,
+                           launch_events=events)
 
     stream = torch.cuda.current_stream(dev)
-    def exchange():
-        # overlapped: start() finishes the previous exchange (device-side wait + apply), then
-        # launches this batch's all-reduce on RCCL's stream, which runs beside the next batch
-        if args.no_overlap:
-            sync.sync()
-        else:
-            sync.start()
-
     for s in range(args.warmup):
         step(s)
-        if sync is not None and (s + 1) % args.sync_every == 0:
-            exchange()
-    if sync is not None:
-        sync.finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    ev = []
     t_start = time.perf_counter()
     for k in range(args.steps):
-        s = args.warmup + k
-        ev[k][0].record(stream)
-        step(s, count=True)
-        ev[k][1].record(stream)
-        if sync is not None and (k + 1) % args.sync_every == 0:
-            exchange()
-    if sync is not None:
-        sync.finish()  # the last exchange is inside the timed region, not overlapped
+        step(args.warmup + k, count=True, events=ev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     kern_ms = [a.elapsed_time(b) for a, b in ev]
+    launches_per_step = len(ev) / args.steps
 
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -321,21 +321,25 @@ def main():
         return
 
     # SURVEY.md §8d algorithmic bytes per pair: the input row read + written and the (1+n) output
-    # rows read + written = 2 (2+n) d 4 (7,168 B at d=128, n=5) when no target is skipped.  A
-    # target whose |dot| >= 6 is skipped (pyx:141) and its row is read but not written, so per
-    # launch: pairs * (3+n) d 4 (reads + the unconditional input write, pyx:149) + updates * d 4.
+    # rows read + written = 2 (2+n) d 4 (7,168 B at d=128, n=5) -- `achieved` / `frac`.  Beside
+    # it, skip-adjusted: a target whose |dot| >= 6 is skipped (pyx:141) and its row is read but
+    # not written, so a launch must move pairs * (3+n) d 4 (reads + the unconditional input write,
+    # pyx:149) + updates * d 4, `updates` counted in-kernel (come_launch_opts.o2_update_count).
     bytes_per_pair_max = 2 * (2 + n) * d * 4
     pairs_rank_step = float(np.mean(pairs_per_step[args.warmup:]))
     updates_rank_step = float(upd_count.item()) / args.steps
+    pairs_launch = pairs_rank_step / launches_per_step
     alg_bytes_step = pairs_rank_step * (3 + n) * d * 4 + updates_rank_step * d * 4
     bytes_per_pair = alg_bytes_step / pairs_rank_step
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
-    achieved = alg_bytes_step / avg_kernel_s / 1e9
+    achieved = pairs_launch * bytes_per_pair_max / avg_kernel_s / 1e9
+    achieved_skip = pairs_launch * bytes_per_pair / avg_kernel_s / 1e9
+    walks_per_launch = B if world == 1 else min(B, sync_walks)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if (tj.get("walks_per_launch") == B and tj.get("dim") == d
+            if (tj.get("walks_per_launch") == walks_per_launch and tj.get("dim") == d
                     and tj.get("negative") == n and tj.get("lr") == args.lr
                     and tj.get("negative_table", "uint32") == table_kind
                     and kernel_name(d, n).replace(" ", "") in
@@ -405,7 +409,12 @@ def main():
             "hot_rows": {"share_threshold": hot_p, "rows": n_hot},
             "negative_table": table_kind,
             "pairs_per_step_per_gpu": pairs_rank_step,
-            "sync_every_steps": args.sync_every if world > 1 else None,
+            "walks_per_launch": walks_per_launch,
+            "sync_walks_per_rank": sync_walks if world > 1 else None,
+            "exchanges_per_step": (-(-B // sync_walks)) if world > 1 else 0,
+            "trainer": "Context2Vec.train_rows (distributed=%s)" % (world > 1),
+            "corpus": "one corpus of %d walks (%d per rank), sharded contiguously" % (
+                world * per_rank, per_rank),
             "parallelism": "walk-shard dp%d + %s delta all-reduce (%s)" % (
                 world, "blocking" if args.no_overlap else "overlapped",
                 "RCCL" if args.dist_backend == "nccl" else args.dist_backend)
@@ -419,8 +428,11 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": kernel_name(d, n),
-            "bytes_per_pair": bytes_per_pair,
-            "bytes_per_pair_no_skip": bytes_per_pair_max,
+            "bytes_per_pair": bytes_per_pair_max,
+            "achieved_skip_adjusted": achieved_skip,
+            "frac_skip_adjusted": achieved_skip / HBM_PEAK_GBS,
+            "bytes_per_pair_skip_adjusted": bytes_per_pair,
+            "pairs_per_launch": pairs_launch,
             "target_updates_per_pair": updates_rank_step / pairs_rank_step,
             "avg_kernel_ms": avg_kernel_s * 1e3,
         },

@@ -13,9 +13,11 @@
                   (8.6 TB/s; 24 algorithmic B per step reported beside it).  CPU baseline: the exact
                   CPython-stream walker (come_walks_reference, native restatement of
                   graph_utils.build_deepwalk_corpus) on host threads.
-Each prints one JSON line.  CPU baselines: the reference's own code on a bounded sample
-(O1: Cython train_o1 via oracle/_ref driven like Node2Vec.train; C4: the reference's numpy
-Community2Vec.train loop restated in oracle/oracle.py and sklearn predict_proba).
+Each prints one JSON line.  CPU baselines on a bounded sample: O1 the builder's Hogwild C
+restatement of train_o1 (oracle/come_oracle_mt.c; reported beside it as the reference-equivalent
+rate, restatement / its calibrated speed-up over the reference's GIL-bound Node2Vec.train,
+profiles/r02_cpu_calibration.json); C4 the reference's numpy Community2Vec.train loop restated in
+oracle/oracle.py and sklearn predict_proba.  The reference itself never reaches the GPU box.
 """
 import argparse
 import json
@@ -75,7 +77,7 @@ def c2(args):
 
     def step():
         tsi.sgns_o1(m.node_embedding, edges, seeds[next(it) % len(seeds)], args.negative, table,
-                    0.2, tsi.MODE_HOGWILD, hot=hot)
+                    args.lr, tsi.MODE_HOGWILD, hot=hot)
     el, ks = timed(step, args.steps, args.warmup)
     pairs = 2 * E
     n, d = args.negative, args.dim
@@ -87,35 +89,41 @@ def c2(args):
         node = m.node_embedding.cpu().numpy().copy()
         threads = orc.usable_cpus()
         try:
-            o1_ratio = "%.1f" % json.load(open(os.path.join(
-                ROOT, "profiles", "r02_cpu_calibration.json")))["o1_ratio_restatement_over_cython"]
+            o1_ratio = float(json.load(open(os.path.join(
+                ROOT, "profiles", "r02_cpu_calibration.json")))["o1_ratio_restatement_over_cython"])
         except (OSError, ValueError, KeyError):
-            o1_ratio = "n/a"
+            o1_ratio = None
         np.random.seed(98)
         cs = tsi.draw_seeds(E)
         t0 = time.time()
         done = pairs_done = 0
         while time.time() - t0 < args.cpu_seconds:
-            p, e = orc.sgns_o1_hogwild(node, g.edges.astype(np.int32), cs, n, m.table_host, 0.2,
+            p, e = orc.sgns_o1_hogwild(node, g.edges.astype(np.int32), cs, n, m.table_host, args.lr,
                                        threads, max(0.1, args.cpu_seconds - (time.time() - t0)))
             pairs_done += p
             done += e
         cel = time.time() - t0
         cpu = {"value": pairs_done / cel, "unit": "pair-updates/s", "cores": threads,
                "kind": "port",
+               "reference_equivalent_value": (pairs_done / cel / o1_ratio) if o1_ratio else None,
+               "reference_equivalent_note": "value / %s = the reference's GIL-bound Node2Vec."
+                                            "train rate on the same cores (calibrated ratio, "
+                                            "profiles/r02_cpu_calibration.json)" % (
+                                                "%.1f" % o1_ratio if o1_ratio else "n/a"),
                "sample": "builder's Hogwild C restatement of train_o1 (oracle/come_oracle_mt.c), "
                          "%d threads taking jobs of 150 edges; %d edges in %.1fs.  The "
                          "reference's Node2Vec.train is GIL-bound (one Python call per edge): "
                          "calibrated in the container, this restatement runs %s x the "
                          "reference's Cython train_o1 at 8 threads "
-                         "(profiles/r02_cpu_calibration.json)" % (threads, done, cel, o1_ratio)}
+                         "(profiles/r02_cpu_calibration.json)" % (
+                             threads, done, cel, "%.1f" % o1_ratio if o1_ratio else "n/a")}
     print(json.dumps({
         "metric": "O1 SGNS pair-updates/sec, SBM 100k nodes / 1M edges, d=128",
         "value": pairs * args.steps / el, "unit": "pair-updates/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True, "dtype": "f32", "data": "synthetic SBM (seed 0)",
         "config": {"workload": "configs[1]/C2: O1 over %d edges of a 100x1000 SBM, d=%d, "
-                               "negative=%d, lr=0.2" % (E, d, n), "hot_rows": n_hot,
+                               "negative=%d, lr=%g" % (E, d, n, args.lr), "hot_rows": n_hot,
                    "negative_table": "uint32" if args.plain_table else "packed"},
         "roofline": {"bound": "hbm", "achieved": bpp * pairs / avg / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": bpp * pairs / avg / 1e9 / HBM_PEAK_GBS,
@@ -325,6 +333,7 @@ def main():
     ap.add_argument("--table-size", type=int, default=100_000_000)
     ap.add_argument("--nodes", type=int, default=1_000_000)
     ap.add_argument("--k", type=int, default=50)
+    ap.add_argument("--lr", type=float, default=0.1)  # lr 0.1 for every config
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hot-p", type=float, default=None,

@@ -33,7 +33,11 @@
 extern "C" {
 #endif
 
-#define COME_ABI_VERSION 1
+/* ABI 2 (this header): come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
+ * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
+ * options "o2_plain_writeback" and "o2_pair_atomics" (ABI 1, ring-kernel Hogwild) were removed and
+ * come_set_option rejects them; o2_kernel = 2 with COME_MODE_HOGWILD returns COME_E_INVALID. */
+#define COME_ABI_VERSION 2
 
 enum {
     COME_OK = 0,
@@ -52,6 +56,15 @@ enum {
 /* Flag OR-ed into `mode` of come_sgns_o2 / come_sgns_o1: `table` points to come_pack_table's
  * packed words (T still the logical number of slots) instead of the uint32 table. */
 #define COME_TABLE_PACKED 0x100
+
+/* Flag OR-ed into `mode` (COME_MODE_HOGWILD): no contended rows -- every row is updated with plain
+ * stores, hot_rows ignored.  Without it a NULL hot_rows makes the library derive the bitmap. */
+#define COME_HOT_NONE 0x200
+
+/* Share of the negative table from which a row counts as contended when the library derives the
+ * bitmap itself: rows holding >= max(1, floor(COME_DEFAULT_HOT_SHARE * T)) slots
+ * (come_amd.training_sdg_inner.DEFAULT_HOT_P; measured in DESIGN.md §3.1). */
+#define COME_DEFAULT_HOT_SHARE 5e-6
 
 int come_abi_version(void);
 const char *come_last_error(void);
@@ -77,6 +90,8 @@ int come_fast_version(void);
  * table       device uint32 [T] negative-sampling table (model.py:97-122), values are rows.
  * negative    0..20;  window >= 0;  1 <= d <= 512.
  * The number of pair updates a batch performs is come_count_o2_pairs() of its walks.
+ * COME_MODE_HOGWILD: the contended rows are derived from `table` per call (as come_sgns_o2_ex with
+ * hot_rows == NULL); OR COME_HOT_NONE into `mode` to treat every row as cold.
  */
 int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,
                  int L, const uint64_t *seeds, int window, int negative, const uint32_t *table,
@@ -220,9 +235,10 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
 
 /* ---- Launch options ----
  * Kernel-selection and grid knobs (0 = automatic unless stated):
- *   o2_kernel           1 = direct kernel, 2 = LDS-ring kernel, 3 = streaming kernel.  Automatic:
- *                       sequential -> ring when it fits; Hogwild -> streaming when the vocabulary
- *                       has >= 32 rows per wavefront in flight (and window <= 31), else direct
+ *   o2_kernel           1 = direct kernel, 2 = LDS-ring kernel (sequential mode only; Hogwild
+ *                       returns COME_E_INVALID), 3 = streaming kernel.  Automatic: sequential ->
+ *                       ring when it fits; Hogwild -> streaming when the vocabulary has >= 32 rows
+ *                       per wavefront in flight (and window <= 31), else direct
  *   o2_blocks_per_cu    O2 grid cap in workgroups per CU
  *   o2_waves_per_block  1 or 2 (automatic 2)
  *   o2_static           1 = static grid-stride walk assignment instead of the device work queue
@@ -272,9 +288,13 @@ int come_set_option(const char *name, int value);
  * hot_rows  device uint32 [ceil(V / 32)] (come_hot_rows), or NULL: in COME_MODE_HOGWILD the rows
  *           whose bit is set are read right before each pair and updated with float-atomic
  *           deltas at the memory side (no concurrent update lost, no stale cached copy); the
- *           other rows are cached per wavefront and written back with plain stores.  Ignored in
- *           COME_MODE_SEQUENTIAL.  With NULL every row is treated as cold, which on graphs with
- *           hubs trains measurably worse than the reference's Hogwild (tests/test_gpu_tierc.py).
+ *           other rows are written back with plain stores.  Ignored in COME_MODE_SEQUENTIAL.
+ *           NULL: the library derives the bitmap from `table` on `stream` before the launch
+ *           (rows holding >= COME_DEFAULT_HOT_SHARE of the table, ~0.1 ms at T = 1e8, into
+ *           library scratch: the first call at a new V allocates, so warm up before capturing a
+ *           stream); pass the bitmap to skip that, or COME_HOT_NONE in `mode` for all-cold (on
+ *           graphs with hubs that trains measurably worse than the reference's Hogwild,
+ *           tests/test_gpu_tierc.py).
  * opts      per-call launch options, or NULL = the process-wide ones. */
 int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,
                     int L, const uint64_t *seeds, int window, int negative,
@@ -288,7 +308,8 @@ int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const int32_t *wa
 int come_hot_rows(const uint32_t *table, uint64_t T, int64_t V, uint64_t min_count,
                   uint32_t *counts, uint32_t *hot_bits, void *stream);
 /* come_sgns_o1 with the contended-row bitmap (Hogwild: an update of a hot endpoint row is a
- * float-atomic delta) and per-call options (opts may be NULL = process-wide). */
+ * float-atomic delta; NULL = derived from the table, COME_HOT_NONE = none, as come_sgns_o2_ex)
+ * and per-call options (opts may be NULL = process-wide). */
 int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
                     const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
                     float lr, int mode, const uint32_t *hot_rows, const come_launch_opts *opts,

@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("COME_LIB_PATH") or os.path.join(HERE, "libcome.so")
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
 TABLE_PACKED = 0x100  # COME_TABLE_PACKED mode flag
+HOT_NONE = 0x200      # COME_HOT_NONE mode flag
+ABI_VERSION = 2       # COME_ABI_VERSION this binding is written for
 
 # Every symbol include/come.h declares (checked by tests/test_capi.py).
 SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
@@ -101,8 +103,9 @@ def lib():
     L.come_write_int_rows.argtypes = [cp, P, i64, i32, i32]
     L.come_save_embedding.argtypes = [cp, P, i64, i32, i64]
     L.come_format_f32.argtypes = [f32, cp]
-    if L.come_abi_version() != 1:
-        raise ComeError("libcome.so ABI version mismatch")
+    if L.come_abi_version() != ABI_VERSION:
+        raise ComeError("libcome.so ABI version %d, this binding needs %d (rebuild the library)"
+                        % (L.come_abi_version(), ABI_VERSION))
     _lib = L
     return L
 

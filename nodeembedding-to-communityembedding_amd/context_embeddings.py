@@ -13,6 +13,15 @@ wavefront per walk (``deterministic=False``: every walk in flight, Hogwild acros
 reference's threads are) or one wavefront in walk order (``deterministic=True``: bit-for-bit the
 reference's workers=1 order; the parity mode).  ``workers`` and ``chunksize`` are accepted for
 signature compatibility.
+
+Multi-GPU (``distributed=True``): the reference's worker pool (:72-109) becomes one
+process per GPU.  Every rank is handed the same corpus, draws the seeds of ALL walks (so the global
+numpy RNG advances exactly as in a one-process run and each walk keeps the seed it would have had),
+trains its contiguous shard, and after every ``sync_walks`` of its walks exchanges its progress
+with the others (come_amd.distributed.DeltaAllReduce: W = W_sync + sum_r (W_r - W_sync), over
+RCCL), the exchange of one batch overlapped with the next batch's launch.  train() ends with a
+blocking exchange: every replica then holds the same tables.  The default period is the one the
+multi-replica tier-C run passes at 8 ranks (tests/test_gpu_tierc.py).
 """
 import logging as log
 import time
@@ -22,21 +31,66 @@ import numpy as np
 from . import training_sdg_inner as tsi
 from .embedding import walks_to_rows
 
+# Walks each rank trains between two exchanges in distributed mode: one full launch per rank
+# (8,192 wavefront slots x 16) -- see DESIGN.md §6 for the held-out loss vs period and N.
+DEFAULT_SYNC_WALKS = 1 << 17
+
+
+def o2_pairs(rows, window):
+    """Pair updates train_o2 performs on walk rows (numpy [P, L] or a CUDA tensor)."""
+    import torch
+    if isinstance(rows, torch.Tensor):
+        lens = (rows >= 0).sum(dim=1).long()
+        return int(torch.where(lens >= window + 1, 2 * window * lens - window * (window + 1),
+                               lens * (lens - 1)).sum())
+    return tsi.count_o2_pairs(rows, window)
+
 
 class Context2Vec(object):
     def __init__(self, lr=0.1, window_size=5, workers=1, negative=5, deterministic=False,
-                 batch_walks=1 << 20):
+                 batch_walks=1 << 20, distributed=False, sync_walks=DEFAULT_SYNC_WALKS,
+                 sparse_sync=False, overlap=True, group=None, hot_share=None, launch_opts=None):
         self.lr = float(lr)
         self.workers = workers
         self.negative = negative
         self.window_size = int(window_size)
         self.deterministic = deterministic
         self.batch_walks = int(batch_walks)
+        self.distributed = bool(distributed)
+        self.sync_walks = int(sync_walks)
+        self.sparse_sync = bool(sparse_sync)
+        self.overlap = bool(overlap)
+        self.group = group
+        self.hot_share = hot_share      # None = training_sdg_inner.DEFAULT_HOT_P
+        self.launch_opts = launch_opts  # per-call come_launch_opts fields (A/B runs)
+        self._exchanges = {}
+        if self.distributed and self.deterministic:
+            raise ValueError("distributed=True trains Hogwild shards; deterministic=True is the "
+                             "one-wavefront parity mode")
+
+    def world(self):
+        from .distributed import world_of
+        return world_of(self.group) if self.distributed else (0, 1)
+
+    def exchange(self, model):
+        """The delta exchange of this model's two tables (cached per table pair), with the tables
+        as they are now as its sync base."""
+        from .distributed import DeltaAllReduce, SparseDeltaAllReduce
+        key = (id(model.node_embedding), id(model.context_embedding))
+        ex = self._exchanges.get(key)
+        if ex is None:
+            cls = SparseDeltaAllReduce if self.sparse_sync else DeltaAllReduce
+            self._exchanges = {key: cls([model.node_embedding, model.context_embedding],
+                                        group=self.group)}
+            return self._exchanges[key]
+        ex.reset()
+        return ex
 
     def train(self, model, paths, total_nodes, alpha=1.0, node_count=0, chunksize=150):
         """Train the context embedding on ``paths`` (iterable of node-id walks, a [P, L] id
         array, or a CUDA id tensor [P, L] with -1 after each walk's end -- converted and trained
-        without leaving the device).  Returns the number of pair updates performed."""
+        without leaving the device).  Returns the number of pair updates performed (by this rank
+        in distributed mode)."""
         import torch
         assert model.node_embedding.dtype == torch.float32
         assert model.context_embedding.dtype == torch.float32
@@ -47,28 +101,70 @@ class Context2Vec(object):
         start = time.time()
         rows = walks_to_rows(model, paths, max_len=tsi.MAX_SENTENCE_LEN)
         seeds = tsi.draw_seeds(rows.shape[0])
-        dev = model.node_embedding.device
-        if isinstance(rows, torch.Tensor):  # device walks: count on the device
-            lens = (rows >= 0).sum(dim=1).long()
-            w_ = self.window_size
-            pairs = int(torch.where(lens >= w_ + 1, 2 * w_ * lens - w_ * (w_ + 1),
-                                    lens * (lens - 1)).sum())
-            n_valid = int(lens.sum())
-        else:
-            pairs = tsi.count_o2_pairs(rows, self.window_size)
-            n_valid = int((rows >= 0).sum())
-        mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
-        hot = None if self.deterministic else model.hot_rows()
-        for s in range(0, rows.shape[0], self.batch_walks):
-            w = rows[s:s + self.batch_walks]
-            w = w.contiguous() if isinstance(w, torch.Tensor) else \
-                torch.from_numpy(np.ascontiguousarray(w)).to(dev)
-            sd = torch.from_numpy(seeds[s:s + self.batch_walks].view(np.int64)).to(dev)
-            tsi.sgns_o2(model.node_embedding, model.context_embedding, w, sd, self.window_size,
-                        self.negative, model.negative_table(), self.lr, alpha, mode, hot=hot)
-        torch.cuda.synchronize(dev)
+        rank, world = self.world()
+        n_batches = None
+        if world > 1:
+            from .distributed import shard_range, shard_walks
+            lo, hi = shard_range(rows.shape[0], 0, world)  # rank 0's shard is the largest
+            n_batches = max(1, -(-(hi - lo) // self.sync_walks))
+            rows, seeds = shard_walks(rows, seeds, rank, world)
+        pairs = o2_pairs(rows, self.window_size)
+        n_valid = int((rows >= 0).sum())
+        self.train_rows(model, rows, seeds, alpha, n_batches=n_batches)
+        if model.node_embedding.is_cuda:
+            torch.cuda.synchronize(model.node_embedding.device)
         elapsed = time.time() - start
         nodes = n_valid + node_count
-        log.info("O2 training on %i nodes (%i pair updates) took %.2fs, %.0f pairs/s",
-                 nodes, pairs, elapsed, pairs / elapsed if elapsed else 0.0)
+        log.info("O2 training on %i nodes (%i pair updates%s) took %.2fs, %.0f pairs/s",
+                 nodes, pairs, " on rank %d of %d" % (rank, world) if world > 1 else "",
+                 elapsed, pairs / elapsed if elapsed else 0.0)
         return pairs
+
+    def train_rows(self, model, rows, seeds, alpha=1.0, n_batches=None, update_count=None,
+                   launch_events=None):
+        """The launches (and, distributed, the exchanges) of train() over walk rows already
+        mapped: ``rows`` [P, L] int32 (numpy or CUDA, -1 = None), ``seeds`` [P] uint64 (numpy)
+        or int64 (CUDA) -- this rank's shard in distributed mode.  ``n_batches``: exchanges to
+        make (every rank must make the same number; default ceil(P / sync_walks)).
+        ``update_count``: CUDA int64 [1] += applied target-row updates (come_launch_opts);
+        ``launch_events``: a list that receives a (start, end) torch.cuda.Event pair recorded
+        around every launch on the launch stream.  Asynchronous: nothing waits for the device
+        except the exchanges' own collectives."""
+        import torch
+        dev = model.node_embedding.device
+        mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
+        hot = None if self.deterministic else model.hot_rows(self.hot_share)
+        table = model.negative_table()
+        rank, world = self.world()
+        ex = self.exchange(model) if world > 1 else None
+        P = rows.shape[0]
+        if ex is None:
+            batch = self.batch_walks
+            n_batches = -(-P // batch)
+        else:
+            batch = self.sync_walks
+            n_batches = n_batches if n_batches is not None else max(1, -(-P // batch))
+        stream = torch.cuda.current_stream(dev) if launch_events is not None else None
+        for b in range(n_batches):
+            w = rows[b * batch:(b + 1) * batch]
+            if w.shape[0]:
+                w = w.contiguous() if isinstance(w, torch.Tensor) else \
+                    torch.from_numpy(np.ascontiguousarray(w, np.int32)).to(dev)
+                sd = seeds[b * batch:(b + 1) * batch]
+                sd = sd if isinstance(sd, torch.Tensor) else \
+                    torch.from_numpy(np.ascontiguousarray(sd, np.uint64).view(np.int64)).to(dev)
+                if launch_events is not None:
+                    ev = (torch.cuda.Event(enable_timing=True),
+                          torch.cuda.Event(enable_timing=True))
+                    ev[0].record(stream)
+                tsi.sgns_o2(model.node_embedding, model.context_embedding, w, sd,
+                            self.window_size, self.negative, table, self.lr, alpha, mode,
+                            opts=self.launch_opts, hot=hot, update_count=update_count)
+                if launch_events is not None:
+                    ev[1].record(stream)
+                    launch_events.append(ev)
+            if ex is not None:
+                if b + 1 < n_batches and self.overlap:
+                    ex.start()  # runs beside the next batch; finished by the next start()
+                else:
+                    ex.sync()   # blocking (the last batch: replicas leave train() identical)

@@ -27,8 +27,14 @@ int64_t *launch_counter(int device, void *stream);
 // Device scratch of at least `bytes` for launches on `stream` (library-owned, one buffer per
 // device, stream and slot, grows on demand: the first call at a larger size allocates, so capture
 // a stream only after a warm-up call of the same shape).
-constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchSlots = 2;
+constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchHotCounts = 2, kScratchHotBits = 3,
+              kScratchSlots = 4;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
+// The contended-row bitmap a Hogwild launch uses when the caller passes none (come_hot.hip):
+// rows holding >= max(1, floor(COME_DEFAULT_HOT_SHARE * T)) slots of `table` (plain uint32 or, with
+// `packed`, come_pack_table's words), written into library scratch on `stream`.
+int derive_hot_rows(int device, const uint32_t *table, uint64_t T, int packed, int64_t V,
+                    void *stream, const uint32_t **bits_out);
 // One consistent snapshot of the process-wide launch options (come_set_option; mutex-guarded).
 // Every entry point takes it once at its start, or uses the caller's come_launch_opts (*_ex).
 come_launch_opts current_opts();

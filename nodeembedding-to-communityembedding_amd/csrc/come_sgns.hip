@@ -90,9 +90,10 @@ static int launch(const come_launch_opts &o, void *fn, void *args, int64_t units
 using namespace come;
 
 static int check_common(int64_t V, int d, int negative, const uint32_t *table, uint64_t T,
-                        int &mode, int &packed) {
+                        int &mode, int &packed, int &hot_none) {
     packed = (mode & COME_TABLE_PACKED) ? 1 : 0;
-    mode &= ~COME_TABLE_PACKED;
+    hot_none = (mode & COME_HOT_NONE) ? 1 : 0;
+    mode &= ~(COME_TABLE_PACKED | COME_HOT_NONE);
     if (packed && ((uintptr_t)table % 16) != 0)
         return set_error(COME_E_INVALID, "packed table must be 16-byte aligned");
     if (V <= 0) return set_error(COME_E_INVALID, "V must be > 0 (got %lld)", (long long)V);
@@ -123,16 +124,27 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
                                const uint32_t *hot_rows, const come_launch_opts *opts,
                                void *stream) {
     const come_launch_opts o = opts ? *opts : current_opts();
-    int packed = 0;
-    int rc = check_common(V, d, negative, table, T, mode, packed);
+    int packed = 0, hot_none = 0;
+    int rc = check_common(V, d, negative, table, T, mode, packed, hot_none);
     if (rc) return rc;
     if (P < 0 || L < 0 || window < 0)
         return set_error(COME_E_INVALID, "P, L and window must be >= 0");
+    if (mode == COME_MODE_HOGWILD && o.o2_kernel == 2)
+        return set_error(COME_E_INVALID, "o2_kernel=2 (LDS ring) is the sequential kernel only");
     if (P == 0 || L == 0) return COME_OK;
     if (!node || !ctx || !walks || !seeds)
         return set_error(COME_E_INVALID, "null node/ctx/walks/seeds pointer");
     if (!aligned_for(node, d) || !aligned_for(ctx, d))
         return set_error(COME_E_INVALID, "node/ctx must be 16-byte aligned for d=%d", d);
+    if (hot_none) {
+        hot_rows = nullptr;
+    } else if (mode == COME_MODE_HOGWILD && hot_rows == nullptr && table != nullptr && T > 0) {
+        int dev = 0;
+        rc = ensure_init(&dev);
+        if (rc) return rc;
+        rc = derive_hot_rows(dev, table, T, packed, V, stream, &hot_rows);
+        if (rc) return rc;
+    }
     O2Args a{node, ctx, walks, seeds, table, V, P, L, d, window, negative, lr, alpha,
              make_fastmod(T), packed, nullptr,
              reinterpret_cast<unsigned long long *>(o.o2_update_count), o.o2_fresh_loads,
@@ -141,6 +153,8 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
     const KernelSet &ks = kernel_set(d, &full);
     const int mi = maxn_index(negative);
     const bool hog = mode == COME_MODE_HOGWILD;
+    // 4-wave workgroups; max_waves 1..3 shrinks them, so max_waves=1 is exactly one wavefront
+    const int wpb = (o.max_waves > 0 && o.max_waves < 4) ? o.max_waves : 4;
     if (hog && (o.o2_kernel == 0 || o.o2_kernel == 3) && window <= 31) {
         // streaming Hogwild kernel: 4-wave workgroups, 8 per CU (= its 8 waves per SIMD at
         // d <= 128, n <= 5; measured 6 / 7 / 8 -> 122 / 115 / 108 ms per C3 launch), device work
@@ -149,8 +163,8 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
         rc = ensure_init(&dev);
         if (rc) return rc;
         const int bpc = o.o2_blocks_per_cu > 0 ? o.o2_blocks_per_cu : 8;
-        const int64_t hcap = hog_max_blocks(o, V, 4, o.rows_per_wave);
-        int64_t blocks = (P + 3) / 4;
+        const int64_t hcap = hog_max_blocks(o, V, wpb, o.rows_per_wave);
+        int64_t blocks = (P + wpb - 1) / wpb;
         if (blocks > (int64_t)num_cus(dev) * bpc) blocks = (int64_t)num_cus(dev) * bpc;
         if (hcap > 0 && blocks > hcap) blocks = hcap;
         // Automatic choice: the streaming kernel reads each pair's rows one pair ahead and runs
@@ -161,9 +175,9 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
         // none at 200k-1M nodes; profiles/r02_ab_hogwild_contention.txt), so small vocabularies
         // run the direct kernel, which reads every row when its pair starts (stable in every
         // run, the same speed there: nearly every row is hot and atomic-bound).
-        if (o.o2_kernel == 3 || V >= kStreamRowsPerWave * 4 * blocks) {
+        if (o.o2_kernel == 3 || V >= kStreamRowsPerWave * wpb * blocks) {
             if (!o.o2_static) a.counter = launch_counter(dev, stream);  // else grid-stride
-            return launch(o, ks.o2_stream[full][mi], &a, P, mode, 4, bpc, 0, stream, hcap);
+            return launch(o, ks.o2_stream[full][mi], &a, P, mode, wpb, bpc, 0, stream, hcap);
         }
     }
     // LDS ring of the sequential kernel: (2w+1) rows + their ids
@@ -172,9 +186,9 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
     const bool ring_ok = rs <= 64 && wave_bytes <= kRingMaxWaveBytes;
     if (!hog && o.o2_kernel != 1 && ring_ok)
         return launch(o, ks.o2_ring[full][mi], &a, P, mode, 1, 1, wave_bytes, stream);
-    return launch(o, ks.o2_direct[full][mi], &a, P, mode, 4,
+    return launch(o, ks.o2_direct[full][mi], &a, P, mode, wpb,
                   o.o2_blocks_per_cu > 0 ? o.o2_blocks_per_cu : 6, 0, stream,
-                  hog ? hog_max_blocks(o, V, 4, o.rows_per_wave) : 0);
+                  hog ? hog_max_blocks(o, V, wpb, o.rows_per_wave) : 0);
 }
 
 extern "C" int come_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks,
@@ -190,8 +204,8 @@ extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edg
                                uint64_t T, float lr, int mode, const uint32_t *hot_rows,
                                const come_launch_opts *opts, void *stream) {
     const come_launch_opts o = opts ? *opts : current_opts();
-    int packed = 0;
-    int rc = check_common(V, d, negative, table, T, mode, packed);
+    int packed = 0, hot_none = 0;
+    int rc = check_common(V, d, negative, table, T, mode, packed, hot_none);
     if (rc) return rc;
     if (E < 0) return set_error(COME_E_INVALID, "E must be >= 0");
     if (E == 0) return COME_OK;
@@ -200,6 +214,15 @@ extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edg
         return set_error(COME_E_INVALID, "O1 supports negative <= 32 (got %d)", negative);
     if (!aligned_for(node, d))
         return set_error(COME_E_INVALID, "node must be 16-byte aligned for d=%d", d);
+    if (hot_none) {
+        hot_rows = nullptr;
+    } else if (mode == COME_MODE_HOGWILD && hot_rows == nullptr && table != nullptr && T > 0) {
+        int dev = 0;
+        rc = ensure_init(&dev);
+        if (rc) return rc;
+        rc = derive_hot_rows(dev, table, T, packed, V, stream, &hot_rows);
+        if (rc) return rc;
+    }
     O1Args a{node,           edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed,
              mode == COME_MODE_HOGWILD ? hot_rows : nullptr};
     int full = 0;

@@ -1035,7 +1035,14 @@ __global__ void __launch_bounds__(256)
                 gk[k] = g;
                 ++nupd;
             }
-            // ---- write-back: negatives (in order; a repeated row ends with its last version) ----
+            // ---- write-back: negatives (in order; a repeated row ends with its last version).
+            // Prefetched copies of the row (the next pair's targets, read before this store):
+            // hot -> + this occurrence's change (g * in; the memory-side atomics of other
+            // wavefronts that the copy was loaded with are kept); cold -> replaced by the stored
+            // value, exactly what a read after the store returns when no other wavefront wrote
+            // the row meanwhile (the cold case; a concurrent plain update in that window is lost,
+            // as in any plain read-modify-write of the reference's Hogwild) -- with walks that
+            // share no row the launch is then bit-identical to the sequential order ----
 #pragma unroll
             for (int k = 1; k <= MAXN; ++k) {
                 if (!upd[k]) continue;
@@ -1044,14 +1051,17 @@ __global__ void __launch_bounds__(256)
                 for (int e = 0; e < VEC; ++e) dlt.v[e] = gk[k] * in.v[e];
                 if (th[k]) dlt.atomic_add(a.ctx + (int64_t)t[k] * d, lane, d);
                 else r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+                const bool hk = th[k];
 #pragma unroll
                 for (int q = 1; q <= MAXN; ++q)
                     if (tn[q] == t[k])
 #pragma unroll
-                        for (int e = 0; e < VEC; ++e) rn[q].v[e] += dlt.v[e];
+                        for (int e = 0; e < VEC; ++e)
+                            rn[q].v[e] = hk ? rn[q].v[e] + dlt.v[e] : r[k].v[e];
                 if (have && nci == t[k] && (npi != ic || nhi))
 #pragma unroll
-                    for (int e = 0; e < VEC; ++e) pos_n.v[e] += dlt.v[e];
+                    for (int e = 0; e < VEC; ++e)
+                        pos_n.v[e] = hk ? pos_n.v[e] + dlt.v[e] : r[k].v[e];
             }
             // ---- the positive: hot -> this pair's change, g * in, now (memory side) and into the
             // prefetched copies; cold -> stored once when the center ends, and its final value

@@ -99,6 +99,70 @@ def all_reduce_sum(tensors, group=None):
     return tensors
 
 
+class TorchComm(object):
+    """The collective the exchanges run on: torch.distributed over `group` ("nccl" = RCCL over
+    xGMI on the GPUs, gloo in the CPU tests)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() \
+            else 1
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        import torch.distributed as dist
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX,
+                               group=self.group, async_op=async_op)
+
+
+class LocalReplicas(object):
+    """`world` replicas in ONE process standing in for `world` ranks -- the multi-replica tier-C
+    runs on one GPU (tests/test_gpu_tierc.py, scripts/tierc_replicas.py) drive N exchange objects
+    through it with exactly the product's arithmetic.  ``comm(r)`` is rank r's collective; the
+    k-th all-reduce of every rank forms one collective, which completes (SUM in rank order) when
+    a handle of it is waited on -- after every rank has contributed.  Only asynchronous
+    all-reduces are supported (a blocking one could not complete in a sequential simulation)."""
+
+    def __init__(self, world):
+        self.world = int(world)
+        self.calls = [[] for _ in range(self.world)]
+        self.done = 0
+
+    def comm(self, rank):
+        return _LocalComm(self, rank)
+
+    def _complete(self, k):
+        while self.done <= k:
+            i = self.done
+            ts = [self.calls[r][i] for r in range(self.world)]
+            acc = ts[0].clone()
+            for t in ts[1:]:
+                acc.add_(t)
+            for t in ts:
+                t.copy_(acc)
+            self.done += 1
+
+
+class _LocalComm(object):
+    def __init__(self, group, rank):
+        self.g, self.rank, self.world = group, rank, group.world
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        if not async_op or op != "sum":
+            raise NotImplementedError("LocalReplicas: asynchronous SUM all-reduces only")
+        k = len(self.g.calls[self.rank])
+        self.g.calls[self.rank].append(t)
+        return _LocalWork(self.g, k)
+
+
+class _LocalWork(object):
+    def __init__(self, group, k):
+        self.g, self.k = group, k
+
+    def wait(self):
+        self.g._complete(self.k)
+
+
 def _fused(t):
     """CUDA fp32 tables with n % 4 == 0 use the fused HIP passes (come_delta_begin/end); CPU
     tensors (gloo tests) use the same arithmetic in torch ops."""
@@ -118,24 +182,32 @@ class DeltaAllReduce(object):
     every rank).  ``bucket_elems`` bounds the size of each all-reduce call (large fp32 buckets:
     xGMI collectives are bandwidth-bound per link, so few big calls beat many small ones)."""
 
-    def __init__(self, tables, group=None, bucket_elems=1 << 26):
+    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None):
         import torch
-        import torch.distributed as dist
         self.tables = list(tables)
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.comm = comm if comm is not None else TorchComm(group)
+        self.world = self.comm.world
         self.bucket = int(bucket_elems)
         self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
         self.dsum = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
         self.down = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
         self.pending = []
 
+    def reset(self):
+        """Make the current tables the sync base (W_sync = W).  Call when every replica holds the
+        same tables but they changed outside the exchange (e.g. another trainer's distributed
+        step), so that change is not counted once per rank as a delta."""
+        self.finish()
+        if self.world > 1:
+            for t, s in zip(self.tables, self.snap):
+                s.copy_(t)
+
     def start(self):
         """Snapshot this rank's delta and launch its asynchronous all-reduce (finishes any
         exchange still pending first)."""
         if self.world == 1:
             return
-        import torch.distributed as dist
         self.finish()
         for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
             if _fused(t):
@@ -147,8 +219,7 @@ class DeltaAllReduce(object):
             flat = ds.view(-1)
             for lo in range(0, flat.numel(), self.bucket):
                 hi = min(lo + self.bucket, flat.numel())
-                self.pending.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM,
-                                                    group=self.group, async_op=True))
+                self.pending.append(self.comm.all_reduce(flat[lo:hi], async_op=True))
 
     def finish(self):
         """Wait for the pending all-reduce (device-side wait on the current stream) and apply
@@ -174,8 +245,13 @@ class DeltaAllReduce(object):
             return
         self.start()
         self.finish()
-        for t, s in zip(self.tables, self.snap):
-            t.copy_(s)
+        self.settle()
+
+    def settle(self):
+        """After a finish() with nothing trained since its start(): W = W_sync exactly."""
+        if self.world > 1:
+            for t, s in zip(self.tables, self.snap):
+                t.copy_(s)
 
     @property
     def busy(self):
@@ -190,17 +266,24 @@ class SparseDeltaAllReduce(object):
     Same start / finish / sync protocol; ``last_rows`` / ``last_bytes`` report the previous
     exchange (rows in the union, bytes all-reduced per rank)."""
 
-    def __init__(self, tables, group=None, bucket_elems=1 << 26):
-        import torch.distributed as dist
+    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None):
         self.tables = list(tables)
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.comm = comm if comm is not None else TorchComm(group)
+        self.world = self.comm.world
         self.bucket = int(bucket_elems)
         self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
         self.pending = []
         self.state = []
         self.last_rows = [0] * len(self.tables)
         self.last_bytes = 0
+
+    def reset(self):
+        """As DeltaAllReduce.reset."""
+        self.finish()
+        if self.world > 1:
+            for t, s in zip(self.tables, self.snap):
+                s.copy_(t)
 
     @staticmethod
     def _flags(t, s):
@@ -218,11 +301,13 @@ class SparseDeltaAllReduce(object):
         if self.world == 1:
             return
         import torch
-        import torch.distributed as dist
         self.finish()
         flags = [self._flags(t, s) for t, s in zip(self.tables, self.snap)]
         flat = torch.cat(flags)
-        dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group)  # union over ranks
+        # union over ranks.  Blocking, and torch.nonzero below waits for the device: start()
+        # returns only after the batch in flight and this flag exchange have finished, so the
+        # row-sparse form does not overlap its exchange with the next batch
+        self.comm.all_reduce(flat, op="max")
         self.state = []
         self.last_bytes = 0
         o = 0
@@ -244,8 +329,7 @@ class SparseDeltaAllReduce(object):
             fl = ds.view(-1)
             for lo in range(0, fl.numel(), self.bucket):
                 hi = min(lo + self.bucket, fl.numel())
-                self.pending.append(dist.all_reduce(fl[lo:hi], op=dist.ReduceOp.SUM,
-                                                    group=self.group, async_op=True))
+                self.pending.append(self.comm.all_reduce(fl[lo:hi], async_op=True))
             self.state.append((idx, ds, do))
             self.last_rows[i] = n
             self.last_bytes += n * d * t.element_size()

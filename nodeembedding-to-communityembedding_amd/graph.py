@@ -100,11 +100,15 @@ def sbm(blocks, block_size, p_in, p_out, seed=0):
     return CSRGraph(V, np.concatenate(parts))
 
 
-def random_walks(g, num_paths, path_length, alpha=0.0, seed=0, device="cuda", starts=None):
+def random_walks(g, num_paths, path_length, alpha=0.0, seed=0, device="cuda", starts=None,
+                 walk_offset=0):
     """Walks [num_paths * V, path_length] of ROW indices (int32 tensor on `device`), -1 after a
     walk stops.  Per pass the start nodes are a fresh permutation of all nodes (graph_utils.py:
     187-192); the walks themselves come from the HIP walker (come_random_walks: uniform
-    neighbour, restart to the first node with probability alpha, Philox stream keyed by seed)."""
+    neighbour, restart to the first node with probability alpha, Philox stream keyed by seed).
+    With ``starts`` given (one walk per entry), ``walk_offset`` is the global index of its first
+    walk: a shard [lo, hi) of a corpus generated with starts[lo:hi], walk_offset=lo equals rows
+    lo..hi-1 of the whole corpus."""
     import torch
     from .graph_utils import device_walks
     dev = torch.device(device)
@@ -116,4 +120,5 @@ def random_walks(g, num_paths, path_length, alpha=0.0, seed=0, device="cuda", st
         starts = torch.cat([torch.randperm(g.V, generator=gen, device=dev)
                             for _ in range(num_paths)])
     starts = torch.as_tensor(starts, device=dev).to(torch.int32).contiguous()
-    return device_walks(rowptr, col, starts, path_length, alpha=alpha, seed=seed)
+    return device_walks(rowptr, col, starts, path_length, alpha=alpha, seed=seed,
+                        walk_offset=walk_offset)

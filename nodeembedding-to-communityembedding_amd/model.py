@@ -64,6 +64,7 @@ class Model(object):
         self.vocab_size = len(self.node_ids)
         self._contiguous = bool(self.node_ids[-1] == self.vocab_size)
         self._vocab = None
+        self._hot_cache = {}  # bitmaps depend on the vocabulary and the table
         self.precalc_sampling()
 
     def precalc_sampling(self):
@@ -136,6 +137,7 @@ class Model(object):
                                              self.table_size, float(power)), "come_make_table")
         self.table_host = table
         self.table = torch.from_numpy(table.view(np.int32)).to(self._torch_device())
+        self._hot_cache = {}
         self.table_packed = None
         if self.table.is_cuda:
             from .training_sdg_inner import pack_table
@@ -144,16 +146,18 @@ class Model(object):
     def hot_rows(self, share=None):
         """Bitmap (CUDA) of the contended rows for Hogwild launches: rows holding at least `share`
         of the negative table (default training_sdg_inner.DEFAULT_HOT_P) -- see come_hot.hip.
-        Cached per share; None when the tables are not on a GPU."""
+        Cached per (share, table buffer, V, T) -- rebuilt after build_vocab_ / make_table; None
+        when the tables are not on a GPU or share <= 0 (no contended rows)."""
         from . import training_sdg_inner as tsi
         share = tsi.DEFAULT_HOT_P if share is None else float(share)
         if not getattr(self.table, "is_cuda", False) or share <= 0:
             return None
         cache = self.__dict__.setdefault("_hot_cache", {})
-        if share not in cache:
-            cache[share] = tsi.hot_rows(self.table, self.vocab_size,
-                                        max(1, int(share * self.table_size)))
-        return cache[share]
+        key = (share, self.table.data_ptr(), int(self.vocab_size), int(self.table.numel()))
+        if key not in cache:
+            cache[key] = tsi.hot_rows(self.table, self.vocab_size,
+                                      max(1, int(share * self.table.numel())))
+        return cache[key]
 
     def negative_table(self):
         """What the trainers pass to the kernels: the exact packed form of the uint32 table

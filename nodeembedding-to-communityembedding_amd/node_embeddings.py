@@ -7,6 +7,12 @@ trains the pairs (edge[0] -> edge[1]) then (edge[1] -> edge[0]) on node_embeddin
 (pyx:444-448).  One launch per pass over the edges (passes stay ordered), one wavefront per edge
 (Hogwild across edges) or, with ``deterministic=True``, one wavefront in edge order (== the
 reference with workers=1).  ``loss`` reproduces :26-31 (-sum log sigma(u.v) over the edges).
+
+Multi-GPU (``distributed=True``): every rank is handed the same edge list, draws
+every edge's seed per pass (the global numpy RNG advances as in one process), trains its
+contiguous shard of each pass and exchanges its node_embedding progress with the other ranks
+after every ``sync_edges`` of its edges and at the end of each pass (DeltaAllReduce over RCCL,
+blocking: an O1 pass is ~1 ms at C2, so the replicas stay one pass apart at most).
 """
 import logging as log
 import time
@@ -17,12 +23,31 @@ from . import training_sdg_inner as tsi
 
 
 class Node2Vec(object):
-    def __init__(self, lr=0.2, workers=1, negative=0, deterministic=False):
+    def __init__(self, lr=0.2, workers=1, negative=0, deterministic=False, distributed=False,
+                 sync_edges=None, group=None):
         self.workers = workers
         self.lr = float(lr)
         self.negative = negative
         self.window_size = 1
         self.deterministic = deterministic
+        self.distributed = bool(distributed)
+        self.sync_edges = None if sync_edges is None else int(sync_edges)
+        self.group = group
+        self._exchanges = {}
+        if self.distributed and self.deterministic:
+            raise ValueError("distributed=True trains Hogwild shards; deterministic=True is the "
+                             "one-wavefront parity mode")
+
+    def exchange(self, model):
+        """Delta exchange of model.node_embedding (cached), based on the table as it is now."""
+        from .distributed import DeltaAllReduce
+        key = id(model.node_embedding)
+        ex = self._exchanges.get(key)
+        if ex is None:
+            self._exchanges = {key: DeltaAllReduce([model.node_embedding], group=self.group)}
+            return self._exchanges[key]
+        ex.reset()
+        return ex
 
     def _edge_rows(self, model, edges):
         """Edges -> [E, 2] int32 rows as prepare_sentences would pass them to train_o1: OOV
@@ -58,17 +83,32 @@ class Node2Vec(object):
         ed = torch.from_numpy(rows).to(dev)
         mode = tsi.MODE_SEQUENTIAL if self.deterministic else tsi.MODE_HOGWILD
         hot = None if self.deterministic else model.hot_rows()
+        from .distributed import shard_range, world_of
+        rank, world = world_of(self.group) if self.distributed else (0, 1)
+        ex = self.exchange(model) if world > 1 else None
         pairs = 0
         for it in range(int(iter)):
             if it > 0 and model.down_sampling:  # every pass draws its own sample (:47)
                 rows = self._edge_rows(model, edges)
                 ed = torch.from_numpy(rows).to(dev)
-            pairs += 2 * int((rows >= 0).all(axis=1).sum())
             seeds = tsi.draw_seeds(rows.shape[0])
+            lo, hi = shard_range(rows.shape[0], rank, world)
+            pairs += 2 * int((rows[lo:hi] >= 0).all(axis=1).sum())
             sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
-            tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.negative_table(),
-                        self.lr, mode, hot=hot)
-        torch.cuda.synchronize(dev)
+            if ex is None:
+                tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.negative_table(),
+                            self.lr, mode, hot=hot)
+                continue
+            # every rank makes the same number of exchanges per pass (rank 0's shard is largest)
+            per = self.sync_edges or max(1, shard_range(rows.shape[0], 0, world)[1])
+            for b in range(max(1, -(-shard_range(rows.shape[0], 0, world)[1] // per))):
+                s, e = min(hi, lo + b * per), min(hi, lo + (b + 1) * per)
+                if e > s:
+                    tsi.sgns_o1(model.node_embedding, ed[s:e], sd[s:e], self.negative,
+                                model.negative_table(), self.lr, mode, hot=hot)
+                ex.sync()
+        if model.node_embedding.is_cuda:
+            torch.cuda.synchronize(dev)
         elapsed = time.time() - start
         log.info("O1 training: %i pair updates took %.2fs, %.0f pairs/s", pairs, elapsed,
                  pairs / elapsed if elapsed else 0.0)

@@ -21,7 +21,8 @@ of one Python call per walk.
 import numpy as np
 
 from . import _lib
-from ._lib import MODE_HOGWILD, MODE_SEQUENTIAL, TABLE_PACKED, check, ptr, stream_handle
+from ._lib import (HOT_NONE, MODE_HOGWILD, MODE_SEQUENTIAL, TABLE_PACKED, check, ptr,
+                   stream_handle)
 
 FAST_VERSION = 0
 MAX_SENTENCE_LEN = 10000
@@ -121,8 +122,29 @@ def hot_rows(table, V, min_count):
     return bits
 
 
+def _hot_arg(hot, node, V):
+    """(pointer, mode flag) for the contended-row argument: "auto" -> NULL (libcome derives the
+    bitmap from the table at DEFAULT_HOT_P), None -> COME_HOT_NONE (every row cold), else a CUDA
+    int32 bitmap of at least ceil(V / 32) words on the tables' device."""
+    import torch
+    if isinstance(hot, str):
+        if hot != "auto":
+            raise ValueError("hot must be a bitmap tensor, None or 'auto'")
+        return None, 0
+    if hot is None:
+        return None, HOT_NONE
+    _require_cuda(hot, "hot", torch.int32)
+    if hot.device != node.device:
+        raise ValueError("hot must be on the tables' device (%s, got %s)" % (node.device,
+                                                                            hot.device))
+    if hot.numel() < (int(V) + 31) // 32:
+        raise ValueError("hot bitmap has %d words, needs ceil(V/32) = %d" % (
+            hot.numel(), (int(V) + 31) // 32))
+    return ptr(hot), 0
+
+
 def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mode=MODE_HOGWILD,
-            opts=None, update_count=None, hot=None):
+            opts=None, update_count=None, hot="auto"):
     """Batched train_o2: every walk of ``walks`` [P, L] (int32 rows, -1 = None) in one launch.
 
     node, ctx: float32 CUDA tensors [V, d], updated in place.  seeds: uint64 (stored as int64)
@@ -132,7 +154,8 @@ def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mod
     options (dict of come_launch_opts fields, see include/come.h); update_count: CUDA int64
     tensor [1] that the launch adds its number of applied target-row updates to; hot: the
     contended-row bitmap of hot_rows() (Hogwild mode: those rows are read per pair and updated
-    with float atomics)."""
+    with float atomics), "auto" (default: derived from `table` by the library per call at
+    DEFAULT_HOT_P) or None (no contended rows: every row updated with plain stores)."""
     import torch
     _require_cuda(node, "node", torch.float32)
     _require_cuda(ctx, "ctx", torch.float32)
@@ -146,18 +169,20 @@ def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mod
     if walks.shape[1] > MAX_SENTENCE_LEN:  # pyx:480 truncates silently; so do we
         walks = walks[:, :MAX_SENTENCE_LEN].contiguous()
     V, d = node.shape
+    hp, hflag = _hot_arg(hot, node, V)
     rc = _lib.lib().come_sgns_o2_ex(ptr(node), ptr(ctx), V, d, ptr(walks), walks.shape[0],
                                     walks.shape[1], ptr(seeds), int(window), int(negative),
-                                    tp, T, float(lr), float(alpha), int(mode) | flag,
-                                    None if hot is None else ptr(hot),
-                                    _opts_arg(opts, update_count), stream_handle(node.device))
+                                    tp, T, float(lr), float(alpha), int(mode) | flag | hflag,
+                                    hp, _opts_arg(opts, update_count),
+                                    stream_handle(node.device))
     check(rc, "come_sgns_o2")
 
 
-def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD, opts=None, hot=None):
+def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD, opts=None, hot="auto"):
     """Batched train_o1 over ``edges`` [E, 2] (int32 rows) in one launch; node updated in place.
     opts: per-call launch options (dict of come_launch_opts fields); hot: contended-row bitmap
-    (hot_rows(); Hogwild: updates of those rows are float-atomic deltas)."""
+    (hot_rows(); Hogwild: updates of those rows are float-atomic deltas), "auto" or None as for
+    sgns_o2."""
     import torch
     _require_cuda(node, "node", torch.float32)
     _require_cuda(edges, "edges", torch.int32)
@@ -166,10 +191,10 @@ def sgns_o1(node, edges, seeds, negative, table, lr, mode=MODE_HOGWILD, opts=Non
     if edges.dim() != 2 or edges.shape[1] != 2 or seeds.shape != (edges.shape[0],):
         raise ValueError("edges must be [E, 2] and seeds [E]")
     V, d = node.shape
+    hp, hflag = _hot_arg(hot, node, V)
     rc = _lib.lib().come_sgns_o1_ex(ptr(node), V, d, ptr(edges), edges.shape[0], ptr(seeds),
-                                    int(negative), tp, T, float(lr), int(mode) | flag,
-                                    None if hot is None else ptr(hot), _opts_arg(opts),
-                                    stream_handle(node.device))
+                                    int(negative), tp, T, float(lr), int(mode) | flag | hflag,
+                                    hp, _opts_arg(opts), stream_handle(node.device))
     check(rc, "come_sgns_o1")
 
 

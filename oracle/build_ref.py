@@ -5,11 +5,14 @@ are read from /root/reference (never copied into the repo), cythonized in a scra
 with the reference's directives (`cython_utils.py:6-8`: boundscheck/wraparound off, cdivision on)
 plus `language_level=2` and `legacy_implicit_noexcept=True` (Cython 3 otherwise inserts
 GIL-acquiring error checks after every BLAS call), compiled with -O3, and ONLY the resulting
-shared object lands in oracle/_ref/ (git-ignored, travels to the GPU box with the snapshot).
+shared object lands in oracle/_ref/ (git-ignored, and listed in .gpurunignore: it never reaches
+the GPU box -- the reference stays in this container).
 
 The module links scipy's bundled BLAS through capsules at import time (pyx:76-86), exactly as the
-reference does.  It is used (a) to generate the golden fixtures under tests/golden/ and (b) as
-`cpu_baseline` kind "reference" in bench.py.  Nothing on the product path imports it.
+reference does.  It is used (a) to generate the golden fixtures under tests/golden/ and (b) to
+calibrate the CPU restatement that bench.py times as `cpu_baseline` kind "port"
+(scripts/calibrate_cpu.py -> profiles/r02_cpu_calibration.json).  Nothing on the product path
+imports it.
 
 Usage:  python oracle/build_ref.py   (no-op with a message when /root/reference is absent)
 """

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round 3 (driver), first GPU pass: the GPU tests (new deterministic stream-kernel tests, C5 and
+# multi-rank tier C), smoke, the default bench line, the multi-rank tier-C curve, and a world-2
+# gloo rehearsal of the trainers' distributed path with both ranks on cuda:0.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+  > gpurun_out/r04a_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r04a_pytest.log; exit 1; }
+tail -3 gpurun_out/r04a_pytest.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04a_smoke.log 2>&1 \
+  || { echo "smoke failed"; tail -20 gpurun_out/r04a_smoke.log; exit 1; }
+tail -1 gpurun_out/r04a_smoke.log
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r04a_bench.json \
+  2> gpurun_out/r04a_bench.err || { echo "bench failed"; tail -20 gpurun_out/r04a_bench.err; exit 1; }
+cat gpurun_out/r04a_bench.json
+timeout -k 10 600 python -u scripts/tierc_replicas.py --fixture c3_1m \
+  --out gpurun_out/r04a_tierc_replicas_c3_1m.json > gpurun_out/r04a_replicas.log 2>&1 \
+  || { echo "replicas failed"; tail -20 gpurun_out/r04a_replicas.log; exit 1; }
+grep world gpurun_out/r04a_replicas.log | head -40
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
+  --dist-backend gloo --all-ranks-device0 --no-cpu-baseline --sync-walks 524288 > gpurun_out/r04a_n2.json \
+  2> gpurun_out/r04a_n2.err || { echo "n2 rehearsal failed"; tail -30 gpurun_out/r04a_n2.err; exit 1; }
+cat gpurun_out/r04a_n2.json

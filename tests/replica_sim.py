@@ -1,0 +1,54 @@
+"""N ranks of the multi-GPU SGNS path simulated in ONE process on one GPU (TEST INFRASTRUCTURE).
+
+Rank r holds its own replica of both tables and trains its contiguous shard of the walks
+(distributed.shard_walks) with the product's Hogwild launch (hot-row bitmap, packed table), one
+launch per ``sync_walks`` walks, exactly as Context2Vec.train_rows does on each rank; after each
+launch the ranks exchange through the product's DeltaAllReduce -- the same fused HIP passes
+(come_delta_begin / come_delta_end) and the same overlapped start / finish protocol -- with the
+RCCL all-reduce replaced by distributed.LocalReplicas (a SUM over the replicas in rank order).
+The last exchange is blocking, so every replica ends equal (as after Context2Vec.train).
+"""
+import numpy as np
+import torch
+
+import come_amd.training_sdg_inner as tsi
+from come_amd.distributed import DeltaAllReduce, LocalReplicas, shard_walks
+
+
+def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negative, table, hot,
+                   lr, alpha=1.0, overlap=True, device="cuda"):
+    """Returns (node, ctx) CUDA tensors of replica 0 after the run (all replicas are equal)."""
+    dev = torch.device(device)
+    group = LocalReplicas(world)
+    reps, exs, shards = [], [], []
+    for r in range(world):
+        n_ = torch.from_numpy(np.ascontiguousarray(node0)).to(dev)
+        c_ = torch.from_numpy(np.ascontiguousarray(ctx0)).to(dev)
+        reps.append((n_, c_))
+        exs.append(DeltaAllReduce([n_, c_], comm=group.comm(r)))
+        w, s = shard_walks(walks, seeds, r, world)
+        shards.append((torch.from_numpy(np.ascontiguousarray(w, np.int32)).to(dev),
+                       torch.from_numpy(np.ascontiguousarray(s, np.uint64).view(np.int64))
+                       .to(dev)))
+    n_batches = max(1, -(-max(w.shape[0] for w, _ in shards) // sync_walks))
+    for b in range(n_batches):
+        last = b + 1 == n_batches
+        for r in range(world):
+            w, s = shards[r]
+            wb, sb = w[b * sync_walks:(b + 1) * sync_walks], s[b * sync_walks:(b + 1) * sync_walks]
+            if wb.shape[0]:
+                tsi.sgns_o2(reps[r][0], reps[r][1], wb.contiguous(), sb.contiguous(), window,
+                            negative, table, lr, alpha, tsi.MODE_HOGWILD, hot=hot)
+            if overlap and not last:
+                exs[r].start()  # finishes the previous exchange, launches this one
+        if overlap and not last:
+            continue
+        for e in exs:           # blocking exchange = start / finish / settle on every rank
+            e.start()
+        for e in exs:
+            e.finish()
+            e.settle()
+    torch.cuda.synchronize(dev)
+    for r in range(1, world):
+        assert torch.equal(reps[r][0], reps[0][0]) and torch.equal(reps[r][1], reps[0][1])
+    return reps[0]

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.come_abi_version() == 1
+    assert L.come_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_invalid_arguments_return_error_without_gpu():
@@ -82,3 +82,19 @@ def test_launch_options_snapshot_and_per_call_struct():
     rc = L.come_sgns_o2_ex(p, p, 0, 128, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p,
                            ctypes.byref(o), p)
     assert rc == -1 and b"V must be" in L.come_last_error()
+
+
+def test_abi2_flags_and_invalid_ring_in_hogwild():
+    """ABI 2: COME_HOT_NONE is accepted as a mode flag; the LDS-ring kernel (o2_kernel=2) is
+    sequential-only and a Hogwild request for it is refused before any device work (P = 0)."""
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    assert L.come_sgns_o2(p, p, 10, 8, p, 0, 10, p, 5, 0, p, 10, 0.1, 1.0,
+                          _lib.MODE_HOGWILD | _lib.HOT_NONE, p) == 0
+    o = _lib.launch_opts(None, o2_kernel=2)
+    rc = L.come_sgns_o2_ex(p, p, 10, 8, p, 0, 10, p, 5, 0, p, 10, 0.1, 1.0, _lib.MODE_HOGWILD,
+                           None, ctypes.byref(o), p)
+    assert rc == -1 and b"sequential" in L.come_last_error()
+    o = _lib.launch_opts(None, o2_kernel=2)
+    assert L.come_sgns_o2_ex(p, p, 10, 8, p, 0, 10, p, 5, 0, p, 10, 0.1, 1.0,
+                             _lib.MODE_SEQUENTIAL, None, ctypes.byref(o), p) == 0

@@ -1,0 +1,118 @@
+"""World-size-2 gloo tests (CPU) of the trainers' multi-GPU path (Context2Vec / Node2Vec with
+distributed=True): corpus sharding, per-walk seeds identical to a one-process run, the global
+numpy RNG advanced identically on every rank, the number and arithmetic of the exchanges, and
+replicas identical at the end.
+
+The kernels need a GPU, so the launches are replaced by an ADDITIVE stand-in (each walk / edge adds
+a fixed function of its rows and seed to the rows it names): with additive updates the delta-sum
+exchange must reproduce the one-process result exactly up to fp32 summation order, which pins the
+orchestration independently of Hogwild statistics (those are tier C, tests/test_gpu_tierc.py)."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fake_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha, mode, hot=None,
+             update_count=None, opts=None):
+    w = walks.long()
+    s = (seeds.long() % 7 + 1).to(torch.float32)
+    for p in range(w.shape[0]):
+        r = w[p][w[p] >= 0]
+        node.index_add_(0, r, torch.full((len(r), node.shape[1]), 1e-3, dtype=torch.float32)
+                        * s[p])
+        ctx.index_add_(0, r, torch.full((len(r), ctx.shape[1]), 2e-3, dtype=torch.float32))
+
+
+def _fake_o1(node, edges, seeds, negative, table, lr, mode, hot=None, opts=None):
+    e = edges.long()
+    s = (seeds.long() % 5 + 1).to(torch.float32)
+    for p in range(e.shape[0]):
+        node.index_add_(0, e[p], torch.full((2, node.shape[1]), 1e-3, dtype=torch.float32) * s[p])
+
+
+def _setup(V=40, d=8):
+    import come_amd.training_sdg_inner as tsi
+    from come_amd.model import Model
+    tsi.sgns_o2 = _fake_o2
+    tsi.sgns_o1 = _fake_o1
+    np.random.seed(11)
+    model = Model((np.arange(1, V + 1), np.arange(1, V + 1) % 5 + 1), size=d, table_size=1000,
+                  k=1, device="cpu")
+    rng = np.random.RandomState(3)
+    walks = rng.randint(1, V + 1, (53, 9))
+    walks[5, 4:] = -1  # a short walk
+    edges = rng.randint(1, V + 1, (31, 2))
+    return model, walks, edges
+
+
+def _run(model, walks, edges, distributed, sync_walks):
+    from come_amd.context_embeddings import Context2Vec
+    from come_amd.node_embeddings import Node2Vec
+    cl = Context2Vec(lr=0.1, window_size=2, negative=3, distributed=distributed,
+                     sync_walks=sync_walks)
+    p1 = cl.train(model, paths=walks, total_nodes=walks.size, alpha=1.0)
+    nl = Node2Vec(lr=0.1, negative=3, distributed=distributed, sync_edges=7)
+    p2 = nl.train(model, edges=edges, iter=2)
+    p3 = cl.train(model, paths=walks, total_nodes=walks.size, alpha=1.0)  # reuses the exchange
+    return p1 + p3, p2
+
+
+def _worker(rank, world, port, out_dir, sync_walks, overlap):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from come_amd import context_embeddings as ce
+    model, walks, edges = _setup()
+    orig = ce.Context2Vec.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.overlap = overlap
+    ce.Context2Vec.__init__ = init
+    p_o2, p_o1 = _run(model, walks, edges, True, sync_walks)
+    np.save(os.path.join(out_dir, "node%d.npy" % rank), model.node_embedding.numpy())
+    np.save(os.path.join(out_dir, "ctx%d.npy" % rank), model.context_embedding.numpy())
+    np.save(os.path.join(out_dir, "rng%d.npy" % rank), np.random.random_sample(4))
+    np.save(os.path.join(out_dir, "pairs%d.npy" % rank), np.array([p_o2, p_o1]))
+    dist.destroy_process_group()
+
+
+def _check(tmp_path, sync_walks, overlap):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), sync_walks, overlap),
+             nprocs=world, join=True)
+    model, walks, edges = _setup()
+    p_o2, p_o1 = _run(model, walks, edges, False, sync_walks)
+    rng = np.random.random_sample(4)
+    ld = lambda n, r: np.load(os.path.join(str(tmp_path), "%s%d.npy" % (n, r)))  # noqa: E731
+    for r in range(world):
+        # replicas identical, equal to the one-process run (additive stand-in), RNG in step
+        np.testing.assert_array_equal(ld("node", r), ld("node", 0))
+        np.testing.assert_array_equal(ld("ctx", r), ld("ctx", 0))
+        np.testing.assert_allclose(ld("node", r), model.node_embedding.numpy(), rtol=0,
+                                   atol=2e-5)
+        np.testing.assert_allclose(ld("ctx", r), model.context_embedding.numpy(), rtol=0,
+                                   atol=2e-5)
+        np.testing.assert_array_equal(ld("rng", r), rng)
+    tot = ld("pairs", 0) + ld("pairs", 1)
+    assert tot[0] == p_o2 and tot[1] == p_o1, (tot, p_o2, p_o1)
+
+
+def test_trainers_distributed_world2_overlapped(tmp_path):
+    _check(tmp_path, sync_walks=5, overlap=True)    # 6 exchanges per train(), overlapped
+
+
+def test_trainers_distributed_world2_blocking_one_sync(tmp_path):
+    _check(tmp_path, sync_walks=1 << 17, overlap=False)  # one exchange per train()

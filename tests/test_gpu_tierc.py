@@ -39,34 +39,7 @@ def dev(a):
     return torch.from_numpy(a).to(DEV)
 
 
-def log_sigmoid(x):
-    return -np.logaddexp(0.0, -x)
-
-
-def sgns_loss(inp, out, rows_in, rows_pos, rows_neg):
-    """Mean held-out SGNS loss (float64, exact sigmoid): -log s(u.c+) - sum_k log s(-u.c_k)."""
-    u = inp[rows_in].astype(np.float64)
-    lp = log_sigmoid(np.einsum("pd,pd->p", u, out[rows_pos].astype(np.float64)))
-    ln = log_sigmoid(-np.einsum("pd,pkd->pk", u, out[rows_neg].astype(np.float64))).sum(1)
-    return float(-(lp + ln).mean())
-
-
-def heldout_o2_pairs(walks, w, n, table, count, seed):
-    """`count` (input row, positive row) window pairs of held-out walks (pyx:494-506: input
-    idx[j], positive idx[i]) with n negatives each drawn from the negative table."""
-    rng = np.random.RandomState(seed)
-    P, L = walks.shape
-    p = rng.randint(0, P, 4 * count)
-    i = rng.randint(0, L, 4 * count)
-    off = rng.randint(1, w + 1, 4 * count) * rng.choice([-1, 1], 4 * count)
-    j = i + off
-    ok = (j >= 0) & (j < L)
-    p, i, j = p[ok], i[ok], j[ok]
-    ci, cj = walks[p, i], walks[p, np.clip(j, 0, L - 1)]
-    ok = (ci >= 0) & (cj >= 0)
-    ci, cj = ci[ok][:count], cj[ok][:count]
-    neg = table[rng.randint(0, len(table), (len(ci), n))].astype(np.int64)
-    return cj, ci, neg
+from tierc_inputs import heldout_o2_pairs, log_sigmoid, sgns_loss  # noqa: E402,F401
 
 
 @pytest.fixture(scope="module")
@@ -344,3 +317,82 @@ def test_karate_nmi_hogwild_within_reference_range():
         np.round(gpu, 3), np.mean(gpu), np.round(cpu, 3), np.mean(cpu)))
     assert 0.48 <= np.mean(gpu) <= 0.73, gpu
     assert abs(np.mean(gpu) - np.mean(cpu)) <= 0.1, (gpu, cpu)
+
+
+# ---- C5's kernel (d = 256, n = 10) ------------------------------------------------------------
+
+def test_o2_hogwild_c5_kernel_shape():
+    """Tier C for configs[4]/C5's kernel, k_sgns_o2_stream<4, true, 10> (d = 256, n = 10), the
+    product's launch (hot-row bitmap, packed table) on a 1M-node Chung-Lu graph (C5's generator
+    and seed), T = 1e8, ONE launch of 131,072 walks (1.0e8 pair updates), lr 0.1: held-out loss
+    of two launches within 1% of the sequential oracle's, a committed fixture
+    (tests/golden/tierc_c5_seq.json, scripts/make_tierc_c5_fixture.py; inputs host-built,
+    tests/tierc_inputs.py C5, matched by digest)."""
+    import json
+    from tierc_inputs import C5_HYPER, c5_inputs
+    fx = json.load(open(os.path.join(GOLDEN, "tierc_c5_seq.json")))
+    x = c5_inputs()
+    assert x.digest == fx["inputs_sha256"], "inputs differ from the fixture's"
+    w, n, lr = C5_HYPER["window"], C5_HYPER["negative"], C5_HYPER["lr"]
+    ri, rp, rn = x.heldout(w, n)
+    l0 = sgns_loss(x.node0, np.zeros_like(x.node0), ri, rp, rn)
+    assert abs(l0 - fx["init_loss"]) < 1e-9
+    tab = dev(x.table)
+    hot = tsi.hot_rows(tab, x.g.V, int(tsi.DEFAULT_HOT_P * len(x.table)))
+    packed = tsi.pack_table(tab)
+    assert packed is not None
+    l_hog = []
+    for _ in range(2):
+        node = dev(x.node0)
+        ctx = torch.zeros_like(node)
+        cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+        tsi.sgns_o2(node, ctx, dev(x.train), dev(x.seeds), w, n, packed, lr, 1.0,
+                    tsi.MODE_HOGWILD, hot=hot, update_count=cnt)
+        torch.cuda.synchronize()
+        l_hog.append(sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn))
+        del node, ctx
+    rel = [abs(v - fx["seq_loss"]) / fx["seq_loss"] for v in l_hog]
+    print("C5 kernel held-out loss: init %.5f  seq (fixture) %.5f  gpu-hogwild %s  max rel %.5f  "
+          "target updates / pair %.3f" % (l0, fx["seq_loss"], " ".join("%.5f" % v for v in l_hog),
+                                         max(rel), int(cnt.item()) / fx["pairs"]))
+    assert fx["seq_loss"] < l0 - 0.5
+    assert max(rel) < 0.01, (l_hog, fx["seq_loss"])  # SURVEY.md §8c tier C
+
+
+# ---- the multi-GPU path: N ranks' delta-sum training (SURVEY.md §8e) --------------------------
+
+@pytest.fixture(scope="module")
+def c3_1m():
+    import json
+    from tierc_inputs import c3_1m_inputs
+    fx = json.load(open(os.path.join(GOLDEN, "tierc_c3_1m_seq.json")))
+    x = c3_1m_inputs()
+    assert x.digest == fx["inputs_sha256"], "inputs differ from the fixture's"
+    ri, rp, rn = x.heldout(5, 5)
+    assert abs(sgns_loss(x.node0, np.zeros_like(x.node0), ri, rp, rn) - fx["init_loss"]) < 1e-9
+    tab = dev(x.table)
+    hot = tsi.hot_rows(tab, x.g.V, int(tsi.DEFAULT_HOT_P * len(x.table)))
+    return fx, x, (ri, rp, rn), tsi.pack_table(tab), hot
+
+
+@pytest.mark.parametrize("world", [8, 4, 2])
+def test_o2_multi_rank_delta_sum_matches_sequential_oracle(c3_1m, world):
+    """`world` ranks simulated on one GPU (tests/replica_sim.py: each rank its own replica and
+    contiguous walk shard, the product's launches, DeltaAllReduce's fused passes and overlapped
+    start / finish protocol, RCCL replaced by a sum over the replicas) at the trainers' default
+    sync period (context_embeddings.DEFAULT_SYNC_WALKS walks per rank between exchanges), over
+    the C3 bench launch's 1,048,576 walks: held-out loss within 1% of the sequential oracle's
+    after the same walks (tests/golden/tierc_c3_1m_seq.json).  The curve over periods and N is
+    scripts/tierc_replicas.py (profiles/r04_tierc_replicas_*.json)."""
+    from come_amd.context_embeddings import DEFAULT_SYNC_WALKS
+    from replica_sim import train_replicas
+    fx, x, (ri, rp, rn), packed, hot = c3_1m
+    node, ctx = train_replicas(x.node0, np.zeros_like(x.node0), x.train, x.seeds, world,
+                               DEFAULT_SYNC_WALKS, 5, 5, packed, hot, 0.1)
+    loss = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
+    del node, ctx
+    torch.cuda.empty_cache()
+    rel = (loss - fx["seq_loss"]) / fx["seq_loss"]
+    print("C3 1M walks, %d ranks x %d walks per exchange: held-out loss %.5f vs seq %.5f "
+          "(rel %+.5f)" % (world, DEFAULT_SYNC_WALKS, loss, fx["seq_loss"], rel))
+    assert abs(rel) < 0.01, (loss, fx["seq_loss"])  # SURVEY.md §8c tier C
