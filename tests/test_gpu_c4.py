@@ -1,0 +1,154 @@
+"""configs[3]/C4 at its own size: K = 50 communities, d = 128, the community
+gradient and the GMM responsibilities at V = 1M rows (checked on sampled rows against float64
+numpy), the EM M-step scatter and whole EM iterations at V = 100k (every row enters the sums)
+against float64 numpy and sklearn.  Reference: ADSCModel/community_embeddings.py:27,36-37,61-78.
+
+Tolerances: the kernels are fp32 MFMA contractions (2 V K d^2 flops in another order) against
+float64: rtol 1e-4 on the community update, 2e-4 abs on responsibilities, 1e-4 of the matrix
+scale on scatter matrices, sklearn's EM within 2e-3 (as tests/test_gpu_gmm.py)."""
+import numpy as np
+import pytest
+import torch
+
+from come_amd import community_embeddings as ce
+from come_amd import gmm
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+K, D = 50, 128
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(DEV)
+
+
+def params(seed, sep=1.0):
+    rng = np.random.RandomState(seed)
+    mu = rng.normal(size=(K, D)) * sep
+    A = rng.normal(size=(K, D, D)) / np.sqrt(D)
+    cov = np.einsum("kij,klj->kil", A, A) * 0.5 + np.eye(D)[None] * 0.5
+    w = rng.dirichlet(np.ones(K) * 3)
+    return w, mu, cov
+
+
+@pytest.fixture(scope="module")
+def c4_rows():
+    """C4's inputs: 1M x 128 N(0, 1) node embeddings (seed 2), pi a
+    row-normalised Dirichlet(1) (seed 3), K = 50 components."""
+    x = np.random.RandomState(2).standard_normal((1_000_000, D)).astype(np.float32)
+    pi = np.random.RandomState(3).dirichlet(np.ones(K), x.shape[0]).astype(np.float32)
+    return x, pi
+
+
+@pytest.mark.parametrize("iters", [1, 2])
+def test_c4_community_grad_k50_1m(c4_rows, iters):
+    """x -= lr clip((beta/K) sum_k pi_ik inv_k (x_i - mu_k), +-5) (:61-78) on all 1M rows; 4,000
+    sampled rows (incl. the first and last row tile) against float64, `iters` rounds."""
+    x0, pi = c4_rows
+    w, mu, cov = params(4)
+    inv = np.linalg.inv(cov.astype(np.float32)).astype(np.float32)  # :36, fp32 inverse
+    beta, lr = 2.0 * K, 0.1  # beta/K = 2: some entries reach the +-5 clip
+    x = t(x0)
+    ce.community_grad(x, t(pi), t(mu), t(inv), beta, lr, iters)
+    got = x.cpu().numpy()
+    rng = np.random.RandomState(5)
+    rows = np.concatenate([np.arange(64), rng.choice(len(x0), 3872, replace=False),
+                           np.arange(len(x0) - 64, len(x0))])
+    ref = x0[rows].astype(np.float64)
+    mu64, inv64, p64 = mu.astype(np.float32).astype(np.float64), inv.astype(np.float64), \
+        pi[rows].astype(np.float64)
+    clipped = 0
+    for _ in range(iters):
+        G = np.zeros_like(ref)
+        for k in range(K):
+            G += p64[:, k:k + 1] * ((ref - mu64[k]) @ inv64[k].T)  # pi_ik inv_k (x_i - mu_k)
+        G *= beta / K
+        clipped += int((np.abs(G) >= 5).sum())
+        ref = ref - np.clip(G, -5, 5) * lr
+    assert clipped > 0
+    step = ref - x0[rows]
+    np.testing.assert_allclose(got[rows] - x0[rows], step, rtol=1e-4,
+                               atol=1e-5 * np.abs(step).max())
+    assert np.isfinite(got).all()
+
+
+def test_c4_responsibilities_k50_1m(c4_rows):
+    """predict_proba (:37) of a K = 50 full-covariance mixture on all 1M rows (come_gmm_resp,
+    sklearn's upper-triangular precision factors) and the EM E-step (come_gmm_estep, + per-row
+    log-sum-exp) on 4,000 sampled rows against the float64 restatement of sklearn."""
+    x0, _ = c4_rows
+    w, mu, cov = params(6, sep=0.3)
+    pc = orc.precision_cholesky(cov)
+    resp = ce.gmm_resp(t(x0), *ce.gmm_resp_params(w, mu, pc, DEV)).cpu().numpy()
+    g = gmm.GaussianMixture(K)
+    g._w, g._mu, g._pc = (torch.as_tensor(a, device=DEV) for a in (w, mu, pc))
+    g._prepare_estep()
+    er, lse = gmm.estep(t(x0), g._e_pc, g._e_mp, g._e_ln)
+    rows = np.random.RandomState(7).choice(len(x0), 4000, replace=False)
+    ref_lr = orc.gmm_log_resp(x0[rows].astype(np.float64), w, mu, cov)
+    np.testing.assert_allclose(resp[rows], np.exp(ref_lr), rtol=0, atol=2e-4)
+    np.testing.assert_allclose(er.cpu().numpy()[rows], np.exp(ref_lr), rtol=0, atol=2e-4)
+    np.testing.assert_allclose(resp.sum(1), 1.0, atol=1e-4)
+    # lse = log sum_k w_k N(x; mu_k, S_k) (its mean is sklearn's lower bound)
+    from scipy.special import logsumexp
+    pc64 = pc
+    ld = np.array([np.log(np.diag(pc64[k])).sum() for k in range(K)])
+    X = x0[rows].astype(np.float64)
+    lp = np.stack([np.log(w[k]) + ld[k] - 0.5 * D * np.log(2 * np.pi)
+                   - 0.5 * ((X @ pc64[k] - mu[k] @ pc64[k]) ** 2).sum(1) for k in range(K)], 1)
+    np.testing.assert_allclose(lse.cpu().numpy()[rows], logsumexp(lp, 1), rtol=2e-5, atol=2e-3)
+
+
+@pytest.fixture(scope="module")
+def c4_100k():
+    rng = np.random.RandomState(8)
+    w, mu, cov = params(9, sep=1.5)
+    lab = rng.choice(K, 100_000, p=w)
+    X = np.empty((100_000, D))
+    for k in range(K):
+        m = lab == k
+        X[m] = rng.multivariate_normal(mu[k], cov[k], m.sum())
+    return X.astype(np.float32), w, mu, cov
+
+
+def test_c4_scatter_k50(c4_100k):
+    """M-step scatter matrices sum_i r_ik (x_i - m_k)(x_i - m_k)^T (come_gmm_scatter, the
+    2-component async MFMA workgroups, K = 50 = 25 pairs) vs float64 for a spread of
+    components, both members of a workgroup pair included."""
+    X, w, mu, cov = c4_100k
+    R = np.random.RandomState(10).dirichlet(np.ones(K), len(X)).astype(np.float32)
+    M = (mu + 0.1).astype(np.float32)
+    S = gmm.scatter(t(X), t(R), t(M)).cpu().numpy()
+    X64 = X.astype(np.float64)
+    for k in (0, 1, 24, 25, 48, 49):
+        Dk = X64 - M[k]
+        ref = (R[:, k, None] * Dk).T @ Dk
+        np.testing.assert_allclose(S[k], ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max(),
+                                   err_msg="component %d" % k)
+
+
+def test_c4_em_iterations_k50_match_sklearn(c4_100k):
+    """Two EM iterations at K = 50, d = 128, V = 100k from fixed initial parameters: the GPU
+    GaussianMixture (E-step + means + scatter + Cholesky) vs sklearn's GaussianMixture (:18,27)
+    with the same weights_init / means_init / precisions_init, tol = 0."""
+    import warnings
+    from sklearn.exceptions import ConvergenceWarning
+    from sklearn.mixture import GaussianMixture as SkGMM
+    X, w, mu, cov = c4_100k
+    rng = np.random.RandomState(11)
+    w0 = np.full(K, 1.0 / K)
+    mu0 = mu + rng.normal(size=mu.shape) * 0.3
+    prec0 = np.stack([np.linalg.inv(c + np.eye(D) * 0.3) for c in cov])
+    kw = dict(n_components=K, covariance_type="full", tol=0.0, reg_covar=1e-5, max_iter=2,
+              weights_init=w0, means_init=mu0, precisions_init=prec0, init_params="random")
+    sk = SkGMM(random_state=0, **kw)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", ConvergenceWarning)
+        sk.fit(X.astype(np.float64))
+    g = gmm.GaussianMixture(random_state=0, **kw).fit(t(X))
+    assert g.n_iter_ == sk.n_iter_ == 2
+    np.testing.assert_allclose(g.weights_, sk.weights_, rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(g.means_, sk.means_, rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(g.covariances_, sk.covariances_, rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(g.lower_bound_, sk.lower_bound_, rtol=1e-4)

@@ -160,7 +160,7 @@ def test_derived_hot_bitmap_matches_explicit():
     table) trains exactly like the explicit come_hot_rows bitmap at DEFAULT_HOT_P, and differs
     from hot=None (COME_HOT_NONE) -- disjoint walks, so every run is deterministic."""
     rng = np.random.RandomState(9)
-    V, d, L, w, n, T = 4096, 128, 16, 3, 0, 10_000_000
+    V, d, L, w, n, T = 1 << 19, 128, 16, 3, 0, 10_000_000  # share 5e-6 = 50 slots: hubs hot
     counts = rng.zipf(1.6, V).clip(1, 10 ** 6)
     table = orc.make_table(counts, T)
     node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
