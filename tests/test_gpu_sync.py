@@ -25,50 +25,37 @@ def test_fused_passes_match_torch_ops():
     assert torch.equal(W2, W + (Dsum - Down))
 
 
-def test_overlapped_protocol_on_cuda_tables(monkeypatch):
-    """Two simulated ranks: the all-reduce is replaced by a sum over both ranks' delta buffers;
-    progress made while the exchange is in flight survives, others' deltas land exactly once."""
-    import torch.distributed as dist
+def test_overlapped_protocol_on_cuda_tables():
+    """Two ranks simulated in one process (distributed.LocalReplicas: the all-reduce is a sum over
+    both ranks' delta buffers) through the fused HIP passes: progress made while the exchange is
+    in flight survives, others' deltas land exactly once; a blocking exchange afterwards leaves
+    both replicas bit-identical."""
     rng = np.random.RandomState(1)
     base = torch.from_numpy(rng.randn(64, 32).astype(np.float32)).to(DEV)
-    ranks = []
-    for r in range(2):
-        t = base.clone()
-        s = cd.DeltaAllReduce.__new__(cd.DeltaAllReduce)
-        s.tables, s.group, s.world, s.bucket = [t], None, 2, 1 << 26
-        s.snap = [t.clone()]
-        s.dsum = [torch.empty_like(t)]
-        s.down = [torch.empty_like(t)]
-        s.pending = []
-        ranks.append(s)
+    group = cd.LocalReplicas(2)
+    ranks = [cd.DeltaAllReduce([base.clone()], comm=group.comm(r)) for r in range(2)]
     d0 = [torch.from_numpy(rng.randn(64, 32).astype(np.float32)).to(DEV) for _ in range(2)]
     for s, d in zip(ranks, d0):
         s.tables[0].add_(d)
-    pend = []
-
-    class Work(object):
-        def wait(self):
-            total = sum(x.clone() for x in pend)
-            for x in pend:
-                x.copy_(total)
-
-    def fake_all_reduce(t, op=None, group=None, async_op=False):
-        pend.append(t)
-        return Work()
-    monkeypatch.setattr(dist, "all_reduce", fake_all_reduce)
     for s in ranks:
         s.start()
     later = [torch.from_numpy(rng.randn(64, 32).astype(np.float32)).to(DEV) for _ in range(2)]
     for s, d in zip(ranks, later):
         s.tables[0].add_(d)
-    ranks[0].pending[0].wait()
     for s in ranks:
-        s.pending = [type("W", (), {"wait": lambda self: None})()]
         s.finish()
     for r, s in enumerate(ranks):
         expect = base + d0[0] + d0[1] + later[r]
         torch.testing.assert_close(s.tables[0], expect, rtol=0, atol=1e-5)
         torch.testing.assert_close(s.snap[0], base + d0[0] + d0[1], rtol=0, atol=1e-5)
+    for s in ranks:
+        s.start()
+    for s in ranks:
+        s.finish()
+        s.settle()
+    assert torch.equal(ranks[0].tables[0], ranks[1].tables[0])
+    torch.testing.assert_close(ranks[0].tables[0], base + d0[0] + d0[1] + later[0] + later[1],
+                               rtol=0, atol=2e-5)
 
 
 def test_row_sparse_passes_match_torch_ops():
