@@ -255,6 +255,8 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
  *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
+ *   gmm_resp_db         GMM E-step / responsibilities at d = 64, 128: 1 = the double-buffered
+ *                       8-wavefront kernel (k_gmm_resp_db), 0 = k_gmm_resp_mfma (bit-identical)
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM
@@ -274,6 +276,7 @@ typedef struct come_launch_opts {
     int walk_staged;
     int o2_fresh_loads;
     int o2_atomic_writeback;
+    int gmm_resp_db;
     uint64_t *o2_update_count;
 } come_launch_opts;
 

@@ -671,6 +671,161 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
     }
 }
 
+// Double-buffered E-step: one 8-wavefront workgroup per CU (256 rows, 32 per wavefront, 2
+// wavefronts per SIMD) holds TWO full padded images of P_k^T (2 x 67.6 KB at d = 128) with their
+// mu_k P_k and params.  While component k's MFMAs read buffer k & 1, P_{k+1}^T is copied
+// global -> LDS into the other buffer (global_load_lds_dwordx4, all 8 wavefronts, no VGPRs): one
+// barrier per component instead of two, and no phase of the triangular skip is short of MFMAs to
+// hide its copy behind (k_gmm_resp_mfma's 112 / 48 split).  Same arithmetic, the
+// same MFMA order per column tile and the same epilogue as k_gmm_resp_mfma: bit-identical output.
+template <int D>
+struct RespDbShape {
+    static constexpr int LD = D + 4;                 // padded image row (conflict-free b128 reads)
+    static constexpr int IMG = D * LD;               // floats per image
+    static constexpr int MP = IMG;                   // mu_k P_k (256 reserved)
+    static constexpr int PAR = IMG + 256;            // lower flag, log_norm (64 reserved)
+    static constexpr int BUF = IMG + 256 + 64;       // floats per buffer
+    static constexpr int LDS = 2 * BUF;              // floats
+    static constexpr int WAVES = 8;
+    static_assert(IMG % 256 == 0, "an image is a whole number of 1 KiB copies");
+};
+
+template <int D>
+__device__ __forceinline__ void resp_db_stage(const RespArgs &a, int k, float *buf, int wid,
+                                              int lane) {
+    using RS = RespDbShape<D>;
+    constexpr int PIECES = RS::IMG / 256;
+    const float *Ptk = a.prec_t + (int64_t)k * D * D;
+#pragma unroll
+    for (int j = 0; j < (PIECES + RS::WAVES - 1) / RS::WAVES; ++j) {
+        const int i = wid + RS::WAVES * j;
+        if (i >= PIECES) break;  // wavefront-uniform
+        const int o = i * 256 + lane * 4;
+        const int c = o / RS::LD, s = o % RS::LD;
+        const int sc = s < D ? s : D - 4;  // padding lanes re-read a valid address
+        __builtin_amdgcn_global_load_lds(Ptk + c * D + sc, buf + i * 256, 16, 0, 0);
+    }
+    if (wid == RS::WAVES - 1) {
+        const int src = lane * 4 < D ? lane * 4 : D - 4;
+        __builtin_amdgcn_global_load_lds(a.mu_prec + (int64_t)k * D + src, buf + RS::MP, 16, 0, 0);
+    } else if (wid == RS::WAVES - 2) {
+        const float *p = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
+                                   : a.log_norm + k;
+        __builtin_amdgcn_global_load_lds(p, buf + RS::PAR, 4, 0, 0);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
+    using RS = RespDbShape<D>;
+    constexpr int CT = D / 32;
+    constexpr int G = D / 8;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t blk0 = (int64_t)blockIdx.x * (32 * RS::WAVES);
+    const int64_t myrow = blk0 + wid * 32 + r;
+    const bool rowok = myrow < a.V;
+    f32x4 xa[G];  // xa[g][i] = x[row][8 g + 4 h + i]
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        xa[g] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (rowok) xa[g] = *reinterpret_cast<const f32x4 *>(a.x + myrow * D + 8 * g + 4 * h);
+    }
+    resp_db_stage<D>(a, 0, sm, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int my_e = 8 * ((r >> 3) & 1) + 4 * ((r >> 2) & 1) + 2 * (r & 1) + ((r >> 1) & 1);
+    const int64_t my_row = blk0 + wid * 32 + (my_e & 3) + 8 * (my_e >> 2) + 4 * h;
+    float run_max = -INFINITY, run_sum = 0.0f;
+    for (int k = 0; k < a.K; ++k) {
+        const float *buf = sm + (k & 1) * RS::BUF;
+        if (k + 1 < a.K) resp_db_stage<D>(a, k + 1, sm + ((k + 1) & 1) * RS::BUF, wid, lane);
+        const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(buf[RS::PAR])) != 0;
+        const float lnk = buf[RS::PAR + 1];
+        f32x16 acc[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
+        {
+            auto fetch = [&](int g, f32x4 (&bv)[CT]) {
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct)
+                    bv[ct] = *reinterpret_cast<const f32x4 *>(buf + (ct * 32 + r) * RS::LD +
+                                                              8 * g + 4 * h);
+            };
+            f32x4 bv[2][CT];
+            fetch(0, bv[0]);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int cur = g & 1;
+                if (g + 1 < G) fetch(g + 1, bv[cur ^ 1]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct) {
+                        if (g >= 4 * (ct + 1) && !full) continue;
+                        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[g][i], bv[cur][ct][i],
+                                                                       acc[ct], 0, 0, 0);
+                    }
+            }
+        }
+        const float *mps = buf + RS::MP;
+        float sq[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            sq[e] = 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const float y = acc[ct][e] - mps[ct * 32 + r];
+                sq[e] = __builtin_fmaf(y, y, sq[e]);
+            }
+        }
+        // reduce-scatter over the 32 columns of a half-wave (as k_gmm_resp_mfma)
+        const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
+        auto scatter_stage = [](float *v, int n, int keep_hi, auto partner) {
+#pragma unroll
+            for (int i = 0; i < n; ++i) {
+                const float keep = keep_hi ? v[i + n] : v[i];
+                const float send = keep_hi ? v[i] : v[i + n];
+                v[i] = keep + partner(send);
+            }
+        };
+        auto dpp = [](float x, auto ctrl) {
+            return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
+                                                              decltype(ctrl)::value, 0xF, 0xF,
+                                                              false));
+        };
+        scatter_stage(sq, 8, b3, [&](float x) { return dpp(x, std::integral_constant<int, 0x140>{}); });
+        scatter_stage(sq, 4, b2, [&](float x) { return dpp(x, std::integral_constant<int, 0x141>{}); });
+        scatter_stage(sq, 2, b0, [&](float x) { return dpp(x, std::integral_constant<int, 0xB1>{}); });
+        scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
+        const float tot = reduce_stage<4>(sq[0]);
+        {
+            const float lp = lnk - 0.5f * tot;
+            if (r < 16 && my_row < a.V) a.resp[my_row * a.K + k] = lp;
+            if (lp > run_max) {
+                run_sum = run_sum * expf(run_max - lp) + 1.0f;
+                run_max = lp;
+            } else {
+                run_sum += expf(lp - run_max);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // buffer k & 1 free; P_{k+1} in the other buffer
+    }
+    if (r < 16 && my_row < a.V) {
+        float *lp = a.resp + my_row * a.K;
+        const float lse = run_max + logf(run_sum);
+        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+        if (a.lse) a.lse[my_row] = lse;
+    }
+}
+
 // ---- GMM M-step scatter matrices -------------------------------------------------------------
 //
 // S_k = sum_i resp[i,k] (x_i - mu_k)(x_i - mu_k)^T, the numerator of sklearn's full covariance
@@ -1390,6 +1545,22 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         rc = hip_error(hipGetLastError(), "k_transpose_sq launch");
         if (rc) return rc;
         a.prec_t = pt;
+        if (current_opts().gmm_resp_db) {
+            const size_t lds_db = sizeof(float) * (size_t)(d == 64 ? RespDbShape<64>::LDS
+                                                                    : RespDbShape<128>::LDS);
+            void (*kdb)(RespArgs) = d == 64 ? k_gmm_resp_db<64> : k_gmm_resp_db<128>;
+            static bool attr_db = false;
+            if (!attr_db) {
+                (void)hipFuncSetAttribute((const void *)k_gmm_resp_db<64>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute((const void *)k_gmm_resp_db<128>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr_db = true;
+            }
+            hipLaunchKernelGGL(kdb, dim3((unsigned)((V + 255) / 256)), dim3(512), lds_db,
+                               (hipStream_t)stream, a);
+            return hip_error(hipGetLastError(), "k_gmm_resp_db launch");
+        }
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(d == 64 ? RespShape<64>::LDS
                                                              : RespShape<128>::LDS);

@@ -26,4 +26,10 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   --dist-backend gloo --all-ranks-device0 --no-cpu-baseline --sync-walks 524288 > gpurun_out/r04a_n2.json \
   2> gpurun_out/r04a_n2.err || { echo "n2 rehearsal failed"; tail -30 gpurun_out/r04a_n2.err; exit 1; }
 cat gpurun_out/r04a_n2.json
+for OPT in 0 1; do
+  timeout -k 10 300 python bench_aux.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline \
+    --opt gmm_resp_db=$OPT > gpurun_out/r04a_c4_db$OPT.json 2> gpurun_out/r04a_c4_db$OPT.err \
+    || { echo "c4 db=$OPT failed"; tail -20 gpurun_out/r04a_c4_db$OPT.err; exit 1; }
+  python -c "import json;j=json.load(open('gpurun_out/r04a_c4_db$OPT.json'));c=j['config'];print('db=$OPT', {k:c[k] for k in c if k.startswith('gmm')})"
+done
 exit $PYTEST_RC

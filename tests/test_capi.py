@@ -77,7 +77,7 @@ def test_launch_options_snapshot_and_per_call_struct():
         _lib.set_option("no_such_knob", 1)
     with pytest.raises(ValueError):
         _lib.launch_opts(no_such_knob=1)
-    assert ctypes.sizeof(_lib.LaunchOpts) == 14 * 4 + 8  # 14 ints, then the pointer
+    assert ctypes.sizeof(_lib.LaunchOpts) == 15 * 4 + 4 + 8  # 15 ints, padding, the pointer
     p = ctypes.c_void_p(0)
     rc = L.come_sgns_o2_ex(p, p, 0, 128, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p,
                            ctypes.byref(o), p)

@@ -233,3 +233,34 @@ def test_community2vec_trains_at_d256():
         ref = orc.community_train(x0.cpu().numpy(), pi, m.centroid.cpu().numpy(),
                                   m.inv_covariance_mat.cpu().numpy(), 0.1, 0.1, 2)
         np.testing.assert_allclose(m.node_embedding.cpu().numpy(), ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("V,K,d", [(1000, 5, 128), (4097, 50, 128), (300, 3, 64), (2049, 9, 64),
+                                   (257, 1, 128)])
+def test_estep_double_buffered_kernel_bit_identical(V, K, d):
+    """k_gmm_resp_db (gmm_resp_db=1: one 8-wavefront workgroup per CU, P_{k+1} staged into the
+    second LDS buffer while component k computes) against k_gmm_resp_mfma: the same MFMA order per
+    column tile and the same epilogue -> bit-identical responsibilities and log-sum-exp, with
+    upper, lower and dense factors mixed and ragged row counts."""
+    from come_amd import _lib
+    rng = np.random.RandomState(V + K + d)
+    X = rng.standard_normal((V, d)).astype(np.float32)
+    P = []
+    for k in range(K):
+        A = rng.standard_normal((d, d)) / np.sqrt(d)
+        P.append(np.triu(A) + 2 * np.eye(d) if k % 3 == 0 else
+                 np.tril(A) + 2 * np.eye(d) if k % 3 == 1 else A + 2 * np.eye(d))
+    P = np.stack(P).astype(np.float32)
+    mp = rng.standard_normal((K, d)).astype(np.float32)
+    ln = np.log(rng.dirichlet(np.ones(K))).astype(np.float32)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev())  # noqa: E731
+    out = []
+    try:
+        for opt in (0, 1):
+            _lib.set_option("gmm_resp_db", opt)
+            r, l = gmm.estep(t(X), t(P), t(mp), t(ln))
+            out.append((r.cpu().numpy(), l.cpu().numpy()))
+    finally:
+        _lib.set_option("gmm_resp_db", 0)
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
