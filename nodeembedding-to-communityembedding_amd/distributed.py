@@ -182,16 +182,22 @@ class DeltaAllReduce(object):
     every rank).  ``bucket_elems`` bounds the size of each all-reduce call (large fp32 buckets:
     xGMI collectives are bandwidth-bound per link, so few big calls beat many small ones)."""
 
-    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None):
+    COMBINES = ("sum", "mean", "touched_mean")
+
+    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum"):
         import torch
+        if combine not in self.COMBINES:
+            raise ValueError("combine must be one of %s" % (self.COMBINES,))
         self.tables = list(tables)
         self.group = group
         self.comm = comm if comm is not None else TorchComm(group)
         self.world = self.comm.world
         self.bucket = int(bucket_elems)
+        self.combine = combine
         self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
         self.dsum = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
         self.down = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
+        self.cnt = None
         self.pending = []
 
     def reset(self):
@@ -209,6 +215,7 @@ class DeltaAllReduce(object):
         if self.world == 1:
             return
         self.finish()
+        self.cnt = [] if self.combine == "touched_mean" else None
         for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
             if _fused(t):
                 _native("come_delta_begin", t, s, ds, do)  # D = Down = W - W_sync
@@ -216,6 +223,10 @@ class DeltaAllReduce(object):
                 ds.copy_(t)
                 ds.sub_(s)                                 # D_own = W - W_sync
                 do.copy_(ds)
+            if self.cnt is not None:  # ranks that changed each row
+                c = (ds.view(ds.shape[0], -1) != 0).any(dim=1).to(ds.dtype)
+                self.cnt.append(c)
+                self.pending.append(self.comm.all_reduce(c, async_op=True))
             flat = ds.view(-1)
             for lo in range(0, flat.numel(), self.bucket):
                 hi = min(lo + self.bucket, flat.numel())
@@ -229,7 +240,12 @@ class DeltaAllReduce(object):
         for w in self.pending:
             w.wait()
         self.pending = []
-        for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
+        for i, (t, s, ds, do) in enumerate(zip(self.tables, self.snap, self.dsum, self.down)):
+            if self.combine == "mean":
+                ds.mul_(1.0 / self.world)
+            elif self.combine == "touched_mean":
+                c = self.cnt[i].clamp_min(1.0)
+                ds.div_(c.view((-1,) + (1,) * (ds.dim() - 1)))
             if _fused(t):
                 _native("come_delta_end", t, s, ds, do)    # S += Dsum; W += Dsum - Down
             else:

@@ -37,17 +37,22 @@ def main(src, tag, kernel=KERNEL):
     write_b = pmc["WRITE_SIZE"] * 1024
     bench = json.load(open(os.path.join(src, "trace_bench.json")))
     cfg = bench["config"]
-    pairs = cfg["pairs_per_step_per_gpu"]
-    alg = bench["roofline"]["bytes_per_pair"] * pairs
+    pairs = bench["roofline"].get("pairs_per_launch", cfg["pairs_per_step_per_gpu"])
+    alg = bench["roofline"]["bytes_per_pair"] * pairs  # SURVEY.md §8d model (7,168 B at C3)
+    alg_skip = bench["roofline"].get("bytes_per_pair_skip_adjusted",
+                                     bench["roofline"]["bytes_per_pair"]) * pairs
     m = re.search(r"d=(\d+), negative=(\d+)", cfg["workload"])
     dim, neg = int(m.group(1)), int(m.group(2))
     ml = re.search(r"lr=([0-9.eE+-]+)", cfg["workload"])
-    traffic = {"kernel": row["Name"], "tag": tag, "walks_per_launch": cfg["walks_per_step_per_gpu"],
+    traffic = {"kernel": row["Name"], "tag": tag,
+               "walks_per_launch": cfg.get("walks_per_launch", cfg["walks_per_step_per_gpu"]),
                "dim": dim, "negative": neg, "lr": float(ml.group(1)) if ml else None,
                "negative_table": cfg.get("negative_table", "uint32"),
                "hbm_bytes_per_launch": read_b + write_b,
                "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
-               "algorithmic_bytes_per_launch": alg, "pairs_per_launch": pairs,
+               "algorithmic_bytes_per_launch": alg,
+               "algorithmic_skip_adjusted_bytes_per_launch": alg_skip,
+               "pairs_per_launch": pairs,
                "rocprof_avg_kernel_ms": avg_ms,
                "bench_event_avg_kernel_ms": bench["roofline"]["avg_kernel_ms"],
                "actual_hbm_GBps": (read_b + write_b) / avg_ms / 1e6,

@@ -25,10 +25,11 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--fixture", choices=["c3_1m", "c3_131k"], default="c3_1m")
+    ap.add_argument("--fixture", choices=["c3_1m", "c3_4m", "c3_131k"], default="c3_1m")
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--periods", default="")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--combines", default="sum")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
@@ -36,12 +37,15 @@ def main():
     from replica_sim import train_replicas
     from tierc_inputs import sgns_loss, heldout_o2_pairs, c3_1m_inputs
     t0 = time.time()
-    if args.fixture == "c3_1m":
-        fx = json.load(open(os.path.join(ROOT, "tests", "golden", "tierc_c3_1m_seq.json")))
-        x = c3_1m_inputs()
+    if args.fixture in ("c3_1m", "c3_4m"):
+        from tierc_inputs import c3_4m_inputs
+        fx = json.load(open(os.path.join(ROOT, "tests", "golden",
+                                         "tierc_%s_seq.json" % args.fixture)))
+        x = c3_1m_inputs() if args.fixture == "c3_1m" else c3_4m_inputs()
         assert x.digest == fx["inputs_sha256"]
         V, table, train, held, node0, seeds = x.g.V, x.table, x.train, x.held, x.node0, x.seeds
-        periods = [1 << 17, 1 << 16, 1 << 15, 1 << 14]
+        periods = [1 << 17, 1 << 16, 1 << 15, 1 << 14] if args.fixture == "c3_1m" else \
+            [1 << 19, 1 << 18, 1 << 17, 1 << 16]
     else:
         from test_gpu_tierc import c3_vocab_inputs, C3_FIXTURE
         fx = json.load(open(C3_FIXTURE))
@@ -63,20 +67,21 @@ def main():
     ctx0 = np.zeros_like(node0)
     out = {"fixture": args.fixture, "walks": int(train.shape[0]), "seq_loss": fx["seq_loss"],
            "init_loss": l0, "overlap": not args.no_overlap, "points": []}
-    for N in [int(v) for v in args.worlds.split(",")]:
-        for p in periods:
+    combines = args.combines.split(",")
+    for comb in combines:
+        for N, p in [(N, p) for N in [int(v) for v in args.worlds.split(",")] for p in periods]:
             per_rank = -(-train.shape[0] // N)
-            if N == 1 and p != periods[0]:
-                continue  # one rank: the period only splits launches
+            if N == 1 and (p != periods[0] or comb != combines[0]):
+                continue  # one rank: no exchange; the period only splits launches
             if p > per_rank and p != periods[0]:
                 continue
             t1 = time.time()
             node, ctx = train_replicas(node0, ctx0, train, seeds, N, min(p, per_rank), w, n,
-                                       packed, hot, lr, overlap=not args.no_overlap)
+                                       packed, hot, lr, overlap=not args.no_overlap, combine=comb)
             l = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
             del node, ctx
             torch.cuda.empty_cache()
-            pt = {"world": N, "sync_walks": min(p, per_rank),
+            pt = {"world": N, "combine": comb, "sync_walks": min(p, per_rank),
                   "exchanges": -(-per_rank // min(p, per_rank)), "loss": l,
                   "rel_to_seq": (l - fx["seq_loss"]) / fx["seq_loss"], "wall_s": time.time() - t1}
             out["points"].append(pt)

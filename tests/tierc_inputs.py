@@ -101,3 +101,14 @@ C3_HYPER = dict(window=5, negative=5, lr=0.1)
 
 def c3_1m_inputs():
     return HostInputs(**C3_1M)
+
+
+# configs[2]/C3 over 4 launches' worth of walks (4,194,304 walks, 3.2e9 pair updates): the
+# multi-GPU path's tier C at sync periods of up to 524,288 walks per rank with 8 ranks; fixture
+# tests/golden/tierc_c3_4m_seq.json (scripts/make_tierc_fixture_host.py c3_4m, ~3 h of one core).
+C3_4M = dict(V=1_000_000, graph_seed=1, d=128, train_walks=1 << 22,
+             walk_streams=(11, 12, 13, 14, 15), pick_seed=7)
+
+
+def c3_4m_inputs():
+    return HostInputs(**C3_4M)
