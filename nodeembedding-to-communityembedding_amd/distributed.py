@@ -182,12 +182,16 @@ class DeltaAllReduce(object):
     every rank).  ``bucket_elems`` bounds the size of each all-reduce call (large fp32 buckets:
     xGMI collectives are bandwidth-bound per link, so few big calls beat many small ones)."""
 
-    COMBINES = ("sum", "mean", "touched_mean")
+    COMBINES = ("sum", "mean", "touched_mean", "hot_mean")
 
-    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum"):
+    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum",
+                 mean_rows=None):
         import torch
         if combine not in self.COMBINES:
             raise ValueError("combine must be one of %s" % (self.COMBINES,))
+        if combine == "hot_mean" and (mean_rows is None or len(mean_rows) != len(tables)):
+            raise ValueError("combine='hot_mean' needs one boolean row mask per table")
+        self.mean_rows = mean_rows
         self.tables = list(tables)
         self.group = group
         self.comm = comm if comm is not None else TorchComm(group)
@@ -246,6 +250,8 @@ class DeltaAllReduce(object):
             elif self.combine == "touched_mean":
                 c = self.cnt[i].clamp_min(1.0)
                 ds.div_(c.view((-1,) + (1,) * (ds.dim() - 1)))
+            elif self.combine == "hot_mean":  # contended rows averaged, the others summed
+                ds[self.mean_rows[i]] *= 1.0 / self.world
             if _fused(t):
                 _native("come_delta_end", t, s, ds, do)    # S += Dsum; W += Dsum - Down
             else:

@@ -76,8 +76,16 @@ def main():
             if p > per_rank and p != periods[0]:
                 continue
             t1 = time.time()
+            cname, mrows = comb, None
+            if comb.startswith("hot_mean"):  # hot_mean[:share] -- rows holding >= share
+                share = float(comb.split(":")[1]) if ":" in comb else tsi.DEFAULT_HOT_P
+                hb = tsi.hot_rows(tab, V, max(1, int(share * len(table))))
+                bits = torch.arange(V, device=dev)
+                mrows = ((hb[bits >> 5] >> (bits & 31)) & 1).bool()
+                cname = "hot_mean"
             node, ctx = train_replicas(node0, ctx0, train, seeds, N, min(p, per_rank), w, n,
-                                       packed, hot, lr, overlap=not args.no_overlap, combine=comb)
+                                       packed, hot, lr, overlap=not args.no_overlap,
+                                       combine=cname, mean_rows=mrows)
             l = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
             del node, ctx
             torch.cuda.empty_cache()

@@ -16,7 +16,7 @@ from come_amd.distributed import DeltaAllReduce, LocalReplicas, shard_walks
 
 
 def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negative, table, hot,
-                   lr, alpha=1.0, overlap=True, device="cuda", combine="sum"):
+                   lr, alpha=1.0, overlap=True, device="cuda", combine="sum", mean_rows=None):
     """Returns (node, ctx) CUDA tensors of replica 0 after the run (all replicas are equal)."""
     dev = torch.device(device)
     group = LocalReplicas(world)
@@ -25,7 +25,8 @@ def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negativ
         n_ = torch.from_numpy(np.ascontiguousarray(node0)).to(dev)
         c_ = torch.from_numpy(np.ascontiguousarray(ctx0)).to(dev)
         reps.append((n_, c_))
-        exs.append(DeltaAllReduce([n_, c_], comm=group.comm(r), combine=combine))
+        exs.append(DeltaAllReduce([n_, c_], comm=group.comm(r), combine=combine,
+                                  mean_rows=None if mean_rows is None else [mean_rows] * 2))
         w, s = shard_walks(walks, seeds, r, world)
         shards.append((torch.from_numpy(np.ascontiguousarray(w, np.int32)).to(dev),
                        torch.from_numpy(np.ascontiguousarray(s, np.uint64).view(np.int64))
