@@ -1042,26 +1042,34 @@ __global__ void __launch_bounds__(256)
             // value, exactly what a read after the store returns when no other wavefront wrote
             // the row meanwhile (the cold case; a concurrent plain update in that window is lost,
             // as in any plain read-modify-write of the reference's Hogwild) -- with walks that
-            // share no row the launch is then bit-identical to the sequential order ----
+            // share no row the launch is then bit-identical to the sequential order.  Written as
+            // two branches: a select form of the same replacement let the compiler wait for the
+            // prefetched copies' loads (826 vs 803 ms per C3 launch; round 2's additive patch for
+            // every row 801 ms, not exact; re-reading the row after the store 803 ms;
+            // profiles/r04_ab_stream_patch.txt) ----
 #pragma unroll
             for (int k = 1; k <= MAXN; ++k) {
                 if (!upd[k]) continue;
-                R dlt;  // this occurrence's change, g * in
+                if (th[k]) {
+                    R dlt;  // this occurrence's change, g * in
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) dlt.v[e] = gk[k] * in.v[e];
-                if (th[k]) dlt.atomic_add(a.ctx + (int64_t)t[k] * d, lane, d);
-                else r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
-                const bool hk = th[k];
+                    for (int e = 0; e < VEC; ++e) dlt.v[e] = gk[k] * in.v[e];
+                    dlt.atomic_add(a.ctx + (int64_t)t[k] * d, lane, d);
 #pragma unroll
-                for (int q = 1; q <= MAXN; ++q)
-                    if (tn[q] == t[k])
+                    for (int q = 1; q <= MAXN; ++q)
+                        if (tn[q] == t[k])
 #pragma unroll
-                        for (int e = 0; e < VEC; ++e)
-                            rn[q].v[e] = hk ? rn[q].v[e] + dlt.v[e] : r[k].v[e];
-                if (have && nci == t[k] && (npi != ic || nhi))
+                            for (int e = 0; e < VEC; ++e) rn[q].v[e] += dlt.v[e];
+                    if (have && nci == t[k] && (npi != ic || nhi))
 #pragma unroll
-                    for (int e = 0; e < VEC; ++e)
-                        pos_n.v[e] = hk ? pos_n.v[e] + dlt.v[e] : r[k].v[e];
+                        for (int e = 0; e < VEC; ++e) pos_n.v[e] += dlt.v[e];
+                } else {
+                    r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+#pragma unroll
+                    for (int q = 1; q <= MAXN; ++q)
+                        if (tn[q] == t[k]) rn[q] = r[k];
+                    if (have && nci == t[k] && (npi != ic || nhi)) pos_n = r[k];
+                }
             }
             // ---- the positive: hot -> this pair's change, g * in, now (memory side) and into the
             // prefetched copies; cold -> stored once when the center ends, and its final value

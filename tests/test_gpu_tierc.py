@@ -319,44 +319,68 @@ def test_karate_nmi_hogwild_within_reference_range():
     assert abs(np.mean(gpu) - np.mean(cpu)) <= 0.1, (gpu, cpu)
 
 
-# ---- C5's kernel (d = 256, n = 10) ------------------------------------------------------------
+# ---- configs[4]/C5 (d = 256, n = 10) -----------------------------------------------------------
 
-def test_o2_hogwild_c5_kernel_shape():
-    """Tier C for configs[4]/C5's kernel, k_sgns_o2_stream<4, true, 10> (d = 256, n = 10), the
-    product's launch (hot-row bitmap, packed table) on a 1M-node Chung-Lu graph (C5's generator
-    and seed), T = 1e8, ONE launch of 131,072 walks (1.0e8 pair updates), lr 0.1: held-out loss
-    of two launches within 1% of the sequential oracle's, a committed fixture
-    (tests/golden/tierc_c5_seq.json, scripts/make_tierc_c5_fixture.py; inputs host-built,
-    tests/tierc_inputs.py C5, matched by digest)."""
-    import json
-    from tierc_inputs import C5_HYPER, c5_inputs
-    fx = json.load(open(os.path.join(GOLDEN, "tierc_c5_seq.json")))
-    x = c5_inputs()
+def c5_launch_losses(x, fx, runs=2):
+    """Held-out losses of `runs` product launches (streaming kernel k_sgns_o2_stream<4, true, 10>,
+    hot-row bitmap, packed table) over the inputs `x`, compared against fixture `fx`."""
+    from tierc_inputs import C5_HYPER, compact_loss
     assert x.digest == fx["inputs_sha256"], "inputs differ from the fixture's"
     w, n, lr = C5_HYPER["window"], C5_HYPER["negative"], C5_HYPER["lr"]
     ri, rp, rn = x.heldout(w, n)
-    l0 = sgns_loss(x.node0, np.zeros_like(x.node0), ri, rp, rn)
-    assert abs(l0 - fx["init_loss"]) < 1e-9
+    l0 = None
     tab = dev(x.table)
     hot = tsi.hot_rows(tab, x.g.V, int(tsi.DEFAULT_HOT_P * len(x.table)))
     packed = tsi.pack_table(tab)
     assert packed is not None
+    walks, seeds = dev(x.train), dev(x.seeds)
+    node0 = torch.from_numpy(x.node0)
     l_hog = []
-    for _ in range(2):
-        node = dev(x.node0)
+    for _ in range(runs):
+        node = node0.to(DEV)
         ctx = torch.zeros_like(node)
-        cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
-        tsi.sgns_o2(node, ctx, dev(x.train), dev(x.seeds), w, n, packed, lr, 1.0,
-                    tsi.MODE_HOGWILD, hot=hot, update_count=cnt)
+        if l0 is None:
+            l0 = compact_loss(node, ctx, ri, rp, rn)
+            assert abs(l0 - fx["init_loss"]) < 1e-9
+        tsi.sgns_o2(node, ctx, walks, seeds, w, n, packed, lr, 1.0, tsi.MODE_HOGWILD, hot=hot)
         torch.cuda.synchronize()
-        l_hog.append(sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn))
+        l_hog.append(compact_loss(node, ctx, ri, rp, rn))
         del node, ctx
-    rel = [abs(v - fx["seq_loss"]) / fx["seq_loss"] for v in l_hog]
-    print("C5 kernel held-out loss: init %.5f  seq (fixture) %.5f  gpu-hogwild %s  max rel %.5f  "
-          "target updates / pair %.3f" % (l0, fx["seq_loss"], " ".join("%.5f" % v for v in l_hog),
-                                         max(rel), int(cnt.item()) / fx["pairs"]))
+        torch.cuda.empty_cache()
+    rel = [(v - fx["seq_loss"]) / fx["seq_loss"] for v in l_hog]
+    print("V=%d: held-out loss init %.5f  seq (fixture) %.5f  gpu-hogwild %s  rel %s" % (
+        x.g.V, l0, fx["seq_loss"], " ".join("%.5f" % v for v in l_hog),
+        " ".join("%+.5f" % r for r in rel)))
     assert fx["seq_loss"] < l0 - 0.5
-    assert max(rel) < 0.01, (l_hog, fx["seq_loss"])  # SURVEY.md §8c tier C
+    return rel
+
+
+def test_o2_hogwild_c5():
+    """Tier C at configs[4]/C5 itself: Chung-Lu 10M nodes / ~100M edges (seed 4), d = 256,
+    n = 10, T = 1e8, lr 0.1, ONE launch of 131,072 walks (1.0e8 pair updates) of the product's
+    Hogwild path: held-out loss of two launches within 1% of the sequential oracle's, a committed
+    fixture (tests/golden/tierc_c5_seq.json, scripts/make_tierc_fixture_host.py c5; inputs
+    host-built, tests/tierc_inputs.py C5, matched by digest)."""
+    import json
+    from tierc_inputs import c5_inputs
+    fx = json.load(open(os.path.join(GOLDEN, "tierc_c5_seq.json")))
+    rel = c5_launch_losses(c5_inputs(), fx)
+    assert max(abs(r) for r in rel) < 0.01, rel  # SURVEY.md §8c tier C
+
+
+def test_o2_hogwild_c5_kernel_on_1m_nodes_regression():
+    """The same kernel on a 1M-node graph of C5's generator, where hubs hold 10x the table share
+    they hold at C5's 10M nodes (the top row 5.0e-4 vs 1.6e-4; rows >= 5e-6 of the table: 9.9% vs
+    1.0% of it).  NOT a tier-C pass: the GPU launch (4,096 wavefronts in flight) trains to a LOWER
+    held-out loss than the sequential oracle, -1.8% (the reference's CPU Hogwild, 7 threads:
+    +0.09%); it shrinks with fewer wavefronts in flight (max_waves 2048 / 1024 / 512: -1.3 / -0.9 /
+    -0.4%, profiles/r04_c5_1m_waves.json) -- stale reads of hub rows under thousands of
+    concurrent updaters.  Guarded here against regressions: within -2.5% .. +1%."""
+    import json
+    from tierc_inputs import c5_1m_inputs
+    fx = json.load(open(os.path.join(GOLDEN, "tierc_c5_1m_seq.json")))
+    rel = c5_launch_losses(c5_1m_inputs(), fx)
+    assert all(-0.025 < r < 0.01 for r in rel), rel
 
 
 # ---- the multi-GPU path: N ranks' delta-sum training (SURVEY.md §8e) --------------------------

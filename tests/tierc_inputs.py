@@ -70,9 +70,16 @@ class HostInputs(object):
         pick = rng.choice(walks.shape[0], train_walks + held_walks, replace=False)
         walks = walks[pick]
         self.train, self.held = walks[:train_walks], walks[train_walks:]
-        self.node0 = rng.uniform(-1, 1, (g.V, d)).astype(np.float32)
+        wbytes = walks.tobytes()
+        del walks
+        # = rng.uniform(-1, 1, (V, d)).astype(np.float32), drawn in row blocks (same stream,
+        # without a V x d float64 temporary: 20 GB at C5's 10M x 256)
+        self.node0 = np.empty((g.V, d), np.float32)
+        for r0 in range(0, g.V, 1 << 20):
+            r1 = min(g.V, r0 + (1 << 20))
+            self.node0[r0:r1] = rng.uniform(-1, 1, (r1 - r0, d))
         self.seeds = rng.randint(0, 2 ** 48, train_walks, dtype=np.int64).astype(np.uint64)
-        self.digest = hashlib.sha256(walks.tobytes() + self.seeds.tobytes() +
+        self.digest = hashlib.sha256(wbytes + self.seeds.tobytes() +
                                      self.node0.tobytes()[:1 << 20] +
                                      self.table.tobytes()[:1 << 20]).hexdigest()
 
@@ -80,16 +87,41 @@ class HostInputs(object):
         return heldout_o2_pairs(self.held, w, n, self.table, count, seed)
 
 
-# configs[4]/C5's kernel (d = 256, n = 10) on a graph the single-core oracle can
-# replay: Chung-Lu 1M nodes (C5's generator and seed, 1/10 of its nodes), T = 1e8, one launch of
-# 131,072 walks (1.0e8 pair updates), lr 0.1, w 5, L 80.
-C5 = dict(V=1_000_000, graph_seed=4, d=256, train_walks=131_072, walk_streams=(41,),
+def compact_loss(node, ctx, rows_in, rows_pos, rows_neg):
+    """sgns_loss with node / ctx given as row-indexable tables (numpy arrays or CUDA tensors):
+    only the rows the held-out pairs name are gathered (and brought to the host), so a 10 GB
+    device table is never copied whole.  Same float64 arithmetic, same value."""
+    ui, ri = np.unique(rows_in, return_inverse=True)
+    uc, rc = np.unique(np.concatenate([rows_pos, rows_neg.ravel()]), return_inverse=True)
+
+    def take(t, rows):
+        if isinstance(t, np.ndarray):
+            return t[rows]
+        import torch
+        return t[torch.from_numpy(rows).to(t.device)].cpu().numpy()
+    inp, out = take(node, ui), take(ctx, uc)
+    npos = len(rows_pos)
+    return sgns_loss(inp, out, ri.reshape(rows_in.shape), rc[:npos],
+                     rc[npos:].reshape(rows_neg.shape))
+
+
+# configs[4]/C5 (SURVEY.md §8d): Chung-Lu 10M nodes / ~100M edges (seed 4), d = 256, n = 10,
+# T = 1e8, lr 0.1, w 5, L 80, one launch of 131,072 walks (1.0e8 pair updates).  C5_1M: the same
+# kernel on a 1M-node graph of the same generator (hubs hold 10x the table share they hold at 10M
+# nodes: the more contended case).
+C5 = dict(V=10_000_000, graph_seed=4, d=256, train_walks=131_072, walk_streams=(41,),
           pick_seed=43)
+C5_1M = dict(V=1_000_000, graph_seed=4, d=256, train_walks=131_072, walk_streams=(41,),
+             pick_seed=43)
 C5_HYPER = dict(window=5, negative=10, lr=0.1)
 
 
 def c5_inputs():
     return HostInputs(**C5)
+
+
+def c5_1m_inputs():
+    return HostInputs(**C5_1M)
 
 
 # configs[2]/C3 at the bench's own launch: the 1M-node graph, one launch of 1,048,576 walks
