@@ -179,6 +179,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1: skip the secondary rows (C2 / C4 / walker via bench_aux.py)")
+    ap.add_argument("--combine", default="touched_mean",
+                    help="N>1: delta exchange combine rule (DeltaAllReduce; DESIGN.md §6)")
     ap.add_argument("--sparse-sync", action="store_true",
                     help="N>1: exchange only the rows some rank changed (SparseDeltaAllReduce)")
     ap.add_argument("--measure-sync", action="store_true",
@@ -265,7 +267,7 @@ def main():
     learner = Context2Vec(lr=args.lr, window_size=w, negative=n, batch_walks=B,
                           distributed=world > 1, sync_walks=sync_walks,
                           sparse_sync=args.sparse_sync, overlap=not args.no_overlap,
-                          hot_share=hot_p, launch_opts=opts)
+                          hot_share=hot_p, launch_opts=opts, combine=args.combine)
     if args.plain_table:
         model.use_packed_table = False
     neg_table = model.negative_table()
@@ -411,6 +413,7 @@ def main():
             "pairs_per_step_per_gpu": pairs_rank_step,
             "walks_per_launch": walks_per_launch,
             "sync_walks_per_rank": sync_walks if world > 1 else None,
+            "exchange_combine": args.combine if world > 1 else None,
             "exchanges_per_step": (-(-B // sync_walks)) if world > 1 else 0,
             "trainer": "Context2Vec.train_rows (distributed=%s)" % (world > 1),
             "corpus": "one corpus of %d walks (%d per rank), sharded contiguously" % (

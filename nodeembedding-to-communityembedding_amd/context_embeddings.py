@@ -17,11 +17,18 @@ signature compatibility.
 Multi-GPU (``distributed=True``): the reference's worker pool (:72-109) becomes one
 process per GPU.  Every rank is handed the same corpus, draws the seeds of ALL walks (so the global
 numpy RNG advances exactly as in a one-process run and each walk keeps the seed it would have had),
-trains its contiguous shard, and after every ``sync_walks`` of its walks exchanges its progress
-with the others (come_amd.distributed.DeltaAllReduce: W = W_sync + sum_r (W_r - W_sync), over
-RCCL), the exchange of one batch overlapped with the next batch's launch.  train() ends with a
-blocking exchange: every replica then holds the same tables.  The default period is the one the
-multi-replica tier-C run passes at 8 ranks (tests/test_gpu_tierc.py).
+trains its contiguous shard, and after every ``sync_walks`` of its walks the ranks all-reduce
+their tables' progress over RCCL (come_amd.distributed.DeltaAllReduce), the exchange of one batch
+overlapped with the next batch's launch.  The combine rule is ``touched_mean``: a row changed by
+k ranks since the last exchange moves by the mean of their k deltas (model averaging restricted
+to the ranks that trained the row, as Spark MLlib's Word2Vec merges partitions).  Summing the
+deltas ("sum", the first-order merge) diverges at lr 0.1: within any practical period a row's
+trajectory saturates on every rank (hub rows take thousands of updates per rank per period), so
+N saturated displacements add up to N times the step (held-out loss 6-100 vs the sequential
+oracle's 2.56 at 2-8 ranks).  Averaging is stable and trains to a LOWER held-out
+loss than the sequential oracle (less SGD noise); it is not the reference's trajectory, which no
+periodic exchange reproduces at this learning rate.  train() ends with a blocking exchange: every
+replica then holds the same tables.
 """
 import logging as log
 import time
@@ -31,8 +38,8 @@ import numpy as np
 from . import training_sdg_inner as tsi
 from .embedding import walks_to_rows
 
-# Walks each rank trains between two exchanges in distributed mode: one full launch per rank
-# (8,192 wavefront slots x 16) -- see DESIGN.md §6 for the held-out loss vs period and N.
+# Walks each rank trains between two exchanges in distributed mode: one full-occupancy launch
+# per rank (8,192 wavefront slots x 16); DESIGN.md §6 has the held-out loss vs period and N.
 DEFAULT_SYNC_WALKS = 1 << 17
 
 
@@ -49,7 +56,8 @@ def o2_pairs(rows, window):
 class Context2Vec(object):
     def __init__(self, lr=0.1, window_size=5, workers=1, negative=5, deterministic=False,
                  batch_walks=1 << 20, distributed=False, sync_walks=DEFAULT_SYNC_WALKS,
-                 sparse_sync=False, overlap=True, group=None, hot_share=None, launch_opts=None):
+                 sparse_sync=False, overlap=True, group=None, hot_share=None, launch_opts=None,
+                 combine="touched_mean"):
         self.lr = float(lr)
         self.workers = workers
         self.negative = negative
@@ -63,6 +71,7 @@ class Context2Vec(object):
         self.group = group
         self.hot_share = hot_share      # None = training_sdg_inner.DEFAULT_HOT_P
         self.launch_opts = launch_opts  # per-call come_launch_opts fields (A/B runs)
+        self.combine = combine          # DeltaAllReduce combine rule
         self._exchanges = {}
         if self.distributed and self.deterministic:
             raise ValueError("distributed=True trains Hogwild shards; deterministic=True is the "
@@ -81,7 +90,7 @@ class Context2Vec(object):
         if ex is None:
             cls = SparseDeltaAllReduce if self.sparse_sync else DeltaAllReduce
             self._exchanges = {key: cls([model.node_embedding, model.context_embedding],
-                                        group=self.group)}
+                                        group=self.group, combine=self.combine)}
             return self._exchanges[key]
         ex.reset()
         return ex

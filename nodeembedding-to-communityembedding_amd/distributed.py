@@ -227,8 +227,8 @@ class DeltaAllReduce(object):
                 ds.copy_(t)
                 ds.sub_(s)                                 # D_own = W - W_sync
                 do.copy_(ds)
-            if self.cnt is not None:  # ranks that changed each row
-                c = (ds.view(ds.shape[0], -1) != 0).any(dim=1).to(ds.dtype)
+            if self.cnt is not None:  # ranks that changed each row (bitwise W != W_sync)
+                c = SparseDeltaAllReduce._flags(t, s)
                 self.cnt.append(c)
                 self.pending.append(self.comm.all_reduce(c, async_op=True))
             flat = ds.view(-1)
@@ -248,7 +248,7 @@ class DeltaAllReduce(object):
             if self.combine == "mean":
                 ds.mul_(1.0 / self.world)
             elif self.combine == "touched_mean":
-                c = self.cnt[i].clamp_min(1.0)
+                c = self.cnt[i].clamp_min(1).to(ds.dtype)
                 ds.div_(c.view((-1,) + (1,) * (ds.dim() - 1)))
             elif self.combine == "hot_mean":  # contended rows averaged, the others summed
                 ds[self.mean_rows[i]] *= 1.0 / self.world
@@ -288,7 +288,10 @@ class SparseDeltaAllReduce(object):
     Same start / finish / sync protocol; ``last_rows`` / ``last_bytes`` report the previous
     exchange (rows in the union, bytes all-reduced per rank)."""
 
-    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None):
+    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum"):
+        if combine not in ("sum", "touched_mean"):
+            raise ValueError("SparseDeltaAllReduce: combine must be 'sum' or 'touched_mean'")
+        self.combine = combine
         self.tables = list(tables)
         self.group = group
         self.comm = comm if comm is not None else TorchComm(group)
@@ -326,10 +329,11 @@ class SparseDeltaAllReduce(object):
         self.finish()
         flags = [self._flags(t, s) for t, s in zip(self.tables, self.snap)]
         flat = torch.cat(flags)
-        # union over ranks.  Blocking, and torch.nonzero below waits for the device: start()
-        # returns only after the batch in flight and this flag exchange have finished, so the
-        # row-sparse form does not overlap its exchange with the next batch
-        self.comm.all_reduce(flat, op="max")
+        # union over ranks (touched_mean: the number of ranks that changed each row).
+        # Blocking, and torch.nonzero below waits for the device: start() returns only after the
+        # batch in flight and this flag exchange have finished, so the row-sparse form does not
+        # overlap its exchange with the next batch
+        self.comm.all_reduce(flat, op="sum" if self.combine == "touched_mean" else "max")
         self.state = []
         self.last_bytes = 0
         o = 0
@@ -352,7 +356,9 @@ class SparseDeltaAllReduce(object):
             for lo in range(0, fl.numel(), self.bucket):
                 hi = min(lo + self.bucket, fl.numel())
                 self.pending.append(self.comm.all_reduce(fl[lo:hi], async_op=True))
-            self.state.append((idx, ds, do))
+            cnt = flat[o - t.shape[0]:o].index_select(0, idx) if self.combine == "touched_mean" \
+                else None
+            self.state.append((idx, ds, do, cnt))
             self.last_rows[i] = n
             self.last_bytes += n * d * t.element_size()
 
@@ -362,10 +368,12 @@ class SparseDeltaAllReduce(object):
         for w in self.pending:
             w.wait()
         self.pending = []
-        for t, s, (idx, ds, do) in zip(self.tables, self.snap, self.state):
+        for t, s, (idx, ds, do, cnt) in zip(self.tables, self.snap, self.state):
             n, d = idx.numel(), t.shape[1]
             if not n:
                 continue
+            if cnt is not None:  # mean over the ranks that changed the row
+                ds.div_(cnt.to(ds.dtype).view(-1, 1))
             if _fused(t) and d % 4 == 0:
                 from . import _lib
                 from ._lib import check, ptr, stream_handle
@@ -382,7 +390,7 @@ class SparseDeltaAllReduce(object):
         if self.world == 1:
             return
         self.start()
-        touched = [idx for idx, _, _ in self.state]
+        touched = [st[0] for st in self.state]
         self.finish()
         for t, s, idx in zip(self.tables, self.snap, touched):
             if idx.numel():
@@ -399,3 +407,17 @@ def reference_delta_sum(w_sync, locals_):
     for w in locals_:
         out += np.asarray(w, np.float64) - np.asarray(w_sync, np.float64)
     return out
+
+
+def reference_touched_mean(w_sync, locals_):
+    """Host restatement of one touched_mean sync for tests: every row gets the mean of the deltas
+    of the ranks that changed it (bitwise), rows nobody changed stay."""
+    s = np.asarray(w_sync, np.float32)
+    out = np.array(s, np.float64, copy=True)
+    tot = np.zeros(s.shape, np.float64)
+    cnt = np.zeros(s.shape[0], np.int64)
+    for w in locals_:
+        w = np.asarray(w, np.float32)
+        tot += w.astype(np.float64) - s.astype(np.float64)
+        cnt += (w.view(np.int32) != s.view(np.int32)).any(axis=1)
+    return out + tot / np.maximum(cnt, 1)[:, None]

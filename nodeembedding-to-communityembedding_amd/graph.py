@@ -15,22 +15,50 @@ import numpy as np
 
 
 class CSRGraph(object):
-    """Undirected simple graph in CSR form over rows 0..V-1 (node id = row + 1)."""
+    """Undirected simple graph in CSR form over rows 0..V-1 (node id = row + 1).  ``device``
+    (a torch CUDA device) runs the sort / unique passes there -- integer operations with the same
+    (stable, sorted) semantics, so the graph is identical to the numpy construction, in seconds
+    instead of minutes at 100M edges."""
 
-    def __init__(self, V, edges_rows):
+    def __init__(self, V, edges_rows, device=None):
+        self.V = int(V)
+        if device is not None:
+            self._build_torch(edges_rows, device)
+            return
         e = np.asarray(edges_rows, np.int64).reshape(-1, 2)
         e = e[e[:, 0] != e[:, 1]]
         a = np.minimum(e[:, 0], e[:, 1])
         b = np.maximum(e[:, 0], e[:, 1])
         key = np.unique(a * V + b)
         a, b = key // V, key % V
-        self.V = int(V)
         self.edges = np.stack([a, b], axis=1)  # unique undirected edges (rows)
         src = np.concatenate([a, b])
         dst = np.concatenate([b, a])
         order = np.argsort(src, kind="stable")
         self.col = dst[order].astype(np.int32)
         self.degree = np.bincount(src, minlength=V).astype(np.int64)
+        self.rowptr = np.zeros(V + 1, np.int64)
+        np.cumsum(self.degree, out=self.rowptr[1:])
+
+    def _build_torch(self, edges_rows, device):
+        import torch
+        V = self.V
+        e = torch.as_tensor(np.asarray(edges_rows, np.int64).reshape(-1, 2), device=device)
+        e = e[e[:, 0] != e[:, 1]]
+        a = torch.minimum(e[:, 0], e[:, 1])
+        b = torch.maximum(e[:, 0], e[:, 1])
+        del e
+        key = torch.unique(a * V + b, sorted=True)
+        a, b = key // V, key % V
+        del key
+        self.edges = torch.stack([a, b], dim=1).cpu().numpy()
+        src = torch.cat([a, b])
+        dst = torch.cat([b, a])
+        del a, b
+        order = torch.sort(src, stable=True).indices
+        self.col = dst[order].to(torch.int32).cpu().numpy()
+        del dst, order
+        self.degree = torch.bincount(src, minlength=V).cpu().numpy().astype(np.int64)
         self.rowptr = np.zeros(V + 1, np.int64)
         np.cumsum(self.degree, out=self.rowptr[1:])
 
@@ -63,16 +91,25 @@ class CSRGraph(object):
         return CSRGraph(len(ids), rows), ids
 
 
-def chung_lu(V, mean_degree, gamma=2.5, seed=1):
+def chung_lu(V, mean_degree, gamma=2.5, seed=1, device=None):
     """Power-law graph with expected degrees w_i ~ (i+1)^(-1/(gamma-1)) scaled to the mean
     degree; V*mean_degree/2 endpoint pairs drawn independently ~ w, self-loops and duplicates
-    removed."""
+    removed.  ``device``: run the searches and sorts with torch on that device (same graph)."""
     rng = np.random.default_rng(seed)
     w = (np.arange(V, dtype=np.float64) + 1.0) ** (-1.0 / (gamma - 1.0))
     w *= mean_degree * V / w.sum()
     cw = np.cumsum(w)
     cw /= cw[-1]
     m = int(V * mean_degree / 2)
+    if device is not None:
+        import torch
+        cwt = torch.as_tensor(cw, device=device)
+        u = torch.searchsorted(cwt, torch.as_tensor(rng.random(m), device=device), right=True)
+        v = torch.searchsorted(cwt, torch.as_tensor(rng.random(m), device=device), right=True)
+        perm = torch.as_tensor(rng.permutation(V), device=device)
+        e = torch.stack([perm[torch.clamp(u, max=V - 1)], perm[torch.clamp(v, max=V - 1)]], 1)
+        del u, v
+        return CSRGraph(V, e.cpu().numpy(), device=device)
     u = np.searchsorted(cw, rng.random(m), side="right")
     v = np.searchsorted(cw, rng.random(m), side="right")
     perm = rng.permutation(V)  # decorrelate degree from node id

@@ -12,7 +12,7 @@ Multi-GPU (``distributed=True``): every rank is handed the same 
 every edge's seed per pass (the global numpy RNG advances as in one process), trains its
 contiguous shard of each pass and exchanges its node_embedding progress with the other ranks
 after every ``sync_edges`` of its edges and at the end of each pass (DeltaAllReduce over RCCL,
-blocking: an O1 pass is ~1 ms at C2, so the replicas stay one pass apart at most).
+combine rule touched_mean as Context2Vec's; blocking: an O1 pass is ~1 ms at C2).
 """
 import logging as log
 import time
@@ -24,7 +24,7 @@ from . import training_sdg_inner as tsi
 
 class Node2Vec(object):
     def __init__(self, lr=0.2, workers=1, negative=0, deterministic=False, distributed=False,
-                 sync_edges=None, group=None):
+                 sync_edges=None, group=None, combine="touched_mean"):
         self.workers = workers
         self.lr = float(lr)
         self.negative = negative
@@ -33,6 +33,7 @@ class Node2Vec(object):
         self.distributed = bool(distributed)
         self.sync_edges = None if sync_edges is None else int(sync_edges)
         self.group = group
+        self.combine = combine  # as Context2Vec's
         self._exchanges = {}
         if self.distributed and self.deterministic:
             raise ValueError("distributed=True trains Hogwild shards; deterministic=True is the "
@@ -44,7 +45,8 @@ class Node2Vec(object):
         key = id(model.node_embedding)
         ex = self._exchanges.get(key)
         if ex is None:
-            self._exchanges = {key: DeltaAllReduce([model.node_embedding], group=self.group)}
+            self._exchanges = {key: DeltaAllReduce([model.node_embedding], group=self.group,
+                                                   combine=self.combine)}
             return self._exchanges[key]
         ex.reset()
         return ex

@@ -11,6 +11,7 @@ only as the checker.  The product package (come_amd) never imports it.
   for covariance_type='full' (sklearn 1.7.2 `_estimate_log_gaussian_prob` +
   `_estimate_weighted_log_prob` + logsumexp normalisation), called by
   community_embeddings.py:37, plus the fp32 np.linalg.inv of :36.
+* Device walker: come_oracle_walks.c restates come_random_walks (Philox stream) bit for bit.
 * Graph + walks: pure-Python restatement of utils/graph_utils.py -- networkx's add_edges_from /
   nodes / edges / degree order (graph_utils.py:60-69) and build_deepwalk_corpus (:172-185) +
   __random_walk__ (:20-46) driven by CPython's own random.Random (the reference's RNG), for small
@@ -40,7 +41,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(HERE, s) for s in ("come_oracle.c", "come_oracle_mt.c")]
+        srcs = [os.path.join(HERE, s) for s in ("come_oracle.c", "come_oracle_mt.c",
+                                                 "come_oracle_walks.c")]
         if not os.path.exists(LIB) or any(
                 os.path.exists(s) and os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs):
             build()
@@ -64,6 +66,7 @@ def lib():
         L.oracle_sgns_o1_hogwild.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, f64,
                                              i64, P]
         L.oracle_sgns_o1_hogwild.restype = i64
+        L.oracle_philox_walks.argtypes = [P, P, i64, P, i64, i32, f32, u64, i64, P, P]
         _lib = L
     return _lib
 
@@ -154,6 +157,19 @@ def sgns_o1_hogwild(node, edges, seeds, negative, table, lr, threads, max_second
                                          table.shape[0], lr, int(threads), float(max_seconds),
                                          int(chunk), _p(done))
     return int(pairs), int(done[0])
+
+
+def philox_walks(rowptr, col, starts, path_length, alpha=0.0, seed=0, walk_offset=0, emit=None):
+    """The device walker's walks (come_random_walks) restated on the host: [P, L] int32."""
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    starts = np.ascontiguousarray(starts, np.int32)
+    out = np.empty((len(starts), int(path_length)), np.int32)
+    em = None if emit is None else np.ascontiguousarray(emit, np.int32)
+    lib().oracle_philox_walks(_p(rowptr), _p(col), len(rowptr) - 1, _p(starts), len(starts),
+                              int(path_length), float(alpha), int(seed) & (2 ** 64 - 1),
+                              int(walk_offset), None if em is None else _p(em), _p(out))
+    return out
 
 
 def usable_cpus():

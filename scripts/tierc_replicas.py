@@ -29,7 +29,9 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--periods", default="")
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--combines", default="sum")
+    ap.add_argument("--combines", default="touched_mean",
+                    help="comma list of combine rules; a '@lrN' suffix trains every rank with lr "
+                         "x N (e.g. mean@lrN)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
@@ -76,15 +78,17 @@ def main():
             if p > per_rank and p != periods[0]:
                 continue
             t1 = time.time()
-            cname, mrows = comb, None
-            if comb.startswith("hot_mean"):  # hot_mean[:share] -- rows holding >= share
-                share = float(comb.split(":")[1]) if ":" in comb else tsi.DEFAULT_HOT_P
+            cname, mrows, lr_r = comb, None, lr
+            if cname.endswith("@lrN"):
+                cname, lr_r = cname[:-4], lr * N
+            if cname.startswith("hot_mean"):  # hot_mean[:share] -- rows holding >= share
+                share = float(cname.split(":")[1]) if ":" in cname else tsi.DEFAULT_HOT_P
                 hb = tsi.hot_rows(tab, V, max(1, int(share * len(table))))
                 bits = torch.arange(V, device=dev)
                 mrows = ((hb[bits >> 5] >> (bits & 31)) & 1).bool()
                 cname = "hot_mean"
             node, ctx = train_replicas(node0, ctx0, train, seeds, N, min(p, per_rank), w, n,
-                                       packed, hot, lr, overlap=not args.no_overlap,
+                                       packed, hot, lr_r, overlap=not args.no_overlap,
                                        combine=cname, mean_rows=mrows)
             l = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
             del node, ctx

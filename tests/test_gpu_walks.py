@@ -143,3 +143,28 @@ def test_staged_output_matches_direct_stores(P, L):
             assert (w[::11] == -1).all()
     finally:
         _lib.set_option("walk_staged", 1)  # the default
+
+
+@pytest.mark.parametrize("alpha,L,offset", [(0.0, 80, 0), (0.15, 33, 5_000_000_123), (1.0, 7, 5)])
+def test_device_walker_bit_exact_vs_cpu_restatement(alpha, L, offset):
+    """come_random_walks (k_random_walks_staged) against its CPU restatement
+    (oracle/come_oracle_walks.c: the same Philox-4x32-10 counters, restart and neighbour picks):
+    identical walks, incl. dead ends (isolated nodes), invalid starts, the restart path, a walk
+    offset beyond 2^32 (the counter's high word) and the emit map."""
+    import torch
+    from come_amd.graph import chung_lu
+    from come_amd.graph_utils import device_walks
+    from oracle import oracle as orc
+    g = chung_lu(50_000, 6.0, gamma=2.5, seed=9)
+    rng = np.random.RandomState(int(alpha * 100) + L)
+    starts = rng.randint(-3, g.V + 3, 20_000).astype(np.int32)
+    emit = rng.permutation(g.V).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
+    for em in (None, emit):
+        got = device_walks(t(g.rowptr), t(g.col), t(starts), L, alpha=alpha, seed=2 ** 40 + 77,
+                           walk_offset=offset, emit=None if em is None else t(em)).cpu().numpy()
+        ref = orc.philox_walks(g.rowptr, g.col, starts, L, alpha, seed=2 ** 40 + 77,
+                               walk_offset=offset, emit=em)
+        np.testing.assert_array_equal(got, ref)
+    assert (ref == -1).any() and (g.degree == 0).any()

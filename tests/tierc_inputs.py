@@ -54,21 +54,39 @@ class HostInputs(object):
     """One tier-C workload built on the host (see the module docstring)."""
 
     def __init__(self, V, graph_seed, d, train_walks, held_walks=20000, T=100_000_000,
-                 walk_streams=(11, 12), pick_seed=7, L=80, mean_degree=20.0):
+                 walk_streams=(11, 12), pick_seed=7, L=80, mean_degree=20.0, walker="host",
+                 walk_seed=0, device=None):
+        """walker "host": full corpus passes of the exact CPython-stream host walker (one per
+        entry of walk_streams), then a random pick of walks; walker "philox": the device walker's
+        stream (come_random_walks, seed walk_seed) from train + held distinct random starts --
+        on `device` when given (a GPU: the product's kernel), else its CPU restatement
+        (oracle/come_oracle_walks.c), identical walks (tests/test_gpu_walks.py)."""
         from oracle import oracle as orc
         from come_amd import graph_utils as gu
         from come_amd.graph import chung_lu
-        g = chung_lu(V, mean_degree, gamma=2.5, seed=graph_seed)
+        g = chung_lu(V, mean_degree, gamma=2.5, seed=graph_seed, device=device)
         self.g = g
         self.table = orc.make_table(g.degree.astype(np.float64), T)
-        gh = gu.Graph(np.arange(1, g.V + 1), g.rowptr, g.col.astype(np.int32), g.degree,
-                      np.zeros((0, 2), np.int32))
-        walks = gu._corpus(gh, [1] * len(walk_streams), L, 0.0,
-                           [random.Random(s) for s in walk_streams], threads=len(walk_streams))
-        walks = np.asarray(walks, np.int32)
         rng = np.random.RandomState(pick_seed)
-        pick = rng.choice(walks.shape[0], train_walks + held_walks, replace=False)
-        walks = walks[pick]
+        if walker == "philox":
+            starts = rng.choice(V, train_walks + held_walks, replace=False).astype(np.int32)
+            if device is not None:
+                import torch
+                walks = gu.device_walks(torch.as_tensor(g.rowptr, device=device),
+                                        torch.as_tensor(g.col, device=device),
+                                        torch.as_tensor(starts, device=device), L, alpha=0.0,
+                                        seed=walk_seed).cpu().numpy()
+            else:
+                walks = orc.philox_walks(g.rowptr, g.col, starts, L, 0.0, seed=walk_seed)
+        else:
+            gh = gu.Graph(np.arange(1, g.V + 1), g.rowptr, g.col.astype(np.int32), g.degree,
+                          np.zeros((0, 2), np.int32))
+            walks = gu._corpus(gh, [1] * len(walk_streams), L, 0.0,
+                               [random.Random(s) for s in walk_streams],
+                               threads=len(walk_streams))
+            walks = np.asarray(walks, np.int32)
+            pick = rng.choice(walks.shape[0], train_walks + held_walks, replace=False)
+            walks = walks[pick]
         self.train, self.held = walks[:train_walks], walks[train_walks:]
         wbytes = walks.tobytes()
         del walks
@@ -109,15 +127,15 @@ def compact_loss(node, ctx, rows_in, rows_pos, rows_neg):
 # T = 1e8, lr 0.1, w 5, L 80, one launch of 131,072 walks (1.0e8 pair updates).  C5_1M: the same
 # kernel on a 1M-node graph of the same generator (hubs hold 10x the table share they hold at 10M
 # nodes: the more contended case).
-C5 = dict(V=10_000_000, graph_seed=4, d=256, train_walks=131_072, walk_streams=(41,),
-          pick_seed=43)
+C5 = dict(V=10_000_000, graph_seed=4, d=256, train_walks=131_072, walker="philox",
+          walk_seed=41, pick_seed=43)
 C5_1M = dict(V=1_000_000, graph_seed=4, d=256, train_walks=131_072, walk_streams=(41,),
              pick_seed=43)
 C5_HYPER = dict(window=5, negative=10, lr=0.1)
 
 
-def c5_inputs():
-    return HostInputs(**C5)
+def c5_inputs(device=None):
+    return HostInputs(device=device, **C5)
 
 
 def c5_1m_inputs():
