@@ -255,8 +255,11 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
  *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
- *   gmm_resp_db         GMM E-step / responsibilities at d = 64, 128: 1 = the double-buffered
- *                       8-wavefront kernel (k_gmm_resp_db), 0 = k_gmm_resp_mfma (bit-identical)
+ *   gmm_resp_db         GMM E-step / responsibilities at d = 64, 128: 0 = k_gmm_resp_mfma;
+ *                       1 = the double-buffered 8-wavefront kernel (k_gmm_resp_db); 2 = the same
+ *                       with the second wave of each SIMD one epilogue late (both bit-identical
+ *                       to 0); 3 = 2 with the accumulators started at -mu_k P_k (own rounding);
+ *                       other values: COME_E_INVALID at the call
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM
@@ -317,6 +320,35 @@ int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edges, int64_t
                     const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
                     float lr, int mode, const uint32_t *hot_rows, const come_launch_opts *opts,
                     void *stream);
+
+/* ---- CPU twins: the same computations on HOST memory with `threads` worker
+ * threads (1..1024), in come_cpu.cpp.  Separate entry points for callers without a GPU; no GPU
+ * entry point calls them (no fallback).  Same argument meaning and validation as the GPU entry
+ * points above; the uint32 table only (no COME_TABLE_PACKED); pairs_out (may be NULL) receives
+ * the pair updates performed.
+ *  come_cpu_sgns_o2 / _o1  COME_MODE_HOGWILD: `threads` workers take jobs of 150 walks (edges) and
+ *                          update the shared tables without locks, as the reference's Context2Vec /
+ *                          Node2Vec worker threads (context_embeddings.py:72-102,
+ *                          node_embeddings.py:58-95); COME_MODE_SEQUENTIAL: the calling thread, in
+ *                          order (= workers=1), bit-identical to come_sgns_o2 / _o1 sequential
+ *                          mode (the same WAVE64 dot order).
+ *  come_cpu_community_grad community_embeddings.py:61-78, k_community_grad's arithmetic order.
+ *  come_cpu_gmm_resp / _estep  community_embeddings.py:37 predict_proba; _estep adds lse_out. */
+int come_cpu_sgns_o2(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,
+                     int L, const uint64_t *seeds, int window, int negative, const uint32_t *table,
+                     uint64_t T, float lr, float alpha, int mode, int threads, int64_t *pairs_out);
+int come_cpu_sgns_o1(float *node, int64_t V, int d, const int32_t *edges, int64_t E,
+                     const uint64_t *seeds, int negative, const uint32_t *table, uint64_t T,
+                     float lr, int mode, int threads, int64_t *pairs_out);
+int come_cpu_community_grad(float *x, int64_t V, int d, const float *pi, const float *mu,
+                            const float *inv_cov, int K, float beta, float lr, int iters,
+                            int threads);
+int come_cpu_gmm_resp(const float *x, int64_t V, int d, const float *prec_chol,
+                      const float *mu_prec, const float *log_norm, int K, float *resp_out,
+                      int threads);
+int come_cpu_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol,
+                       const float *mu_prec, const float *log_norm, int K, float *resp_out,
+                       float *lse_out, int threads);
 
 /* ---- Host helpers ---- */
 

@@ -26,7 +26,8 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_gmm_estep", "come_gmm_scatter", "come_pack_table",
            "come_delta_begin", "come_delta_end", "come_get_options", "come_sgns_o2_ex",
            "come_sgns_o1_ex", "come_hot_rows", "come_lcg_table_draws", "come_delta_flags",
-           "come_delta_gather", "come_delta_scatter")
+           "come_delta_gather", "come_delta_scatter", "come_cpu_sgns_o2", "come_cpu_sgns_o1",
+           "come_cpu_community_grad", "come_cpu_gmm_resp", "come_cpu_gmm_estep")
 
 OPTION_FIELDS = ("o2_kernel", "o2_blocks_per_cu", "o2_waves_per_block",
                  "o2_static", "rows_per_wave", "o1_rows_per_wave",
@@ -94,6 +95,12 @@ def lib():
     L.come_delta_gather.argtypes = [P, P, P, i64, i32, P, P, P]
     L.come_delta_scatter.argtypes = [P, P, P, i64, i32, P, P, P]
     L.come_sgns_o1_ex.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, P, P, P]
+    L.come_cpu_sgns_o2.argtypes = [P, P, i64, i32, P, i64, i32, P, i32, i32, P, u64, f32, f32,
+                                   i32, i32, P]
+    L.come_cpu_sgns_o1.argtypes = [P, i64, i32, P, i64, P, i32, P, u64, f32, i32, i32, P]
+    L.come_cpu_community_grad.argtypes = [P, i64, i32, P, P, P, i32, f32, f32, i32, i32]
+    L.come_cpu_gmm_resp.argtypes = [P, i64, i32, P, P, P, i32, P, i32]
+    L.come_cpu_gmm_estep.argtypes = [P, i64, i32, P, P, P, i32, P, P, i32]
     cp = ctypes.c_char_p
     L.come_random_walks.argtypes = [P, P, i64, P, i64, i32, f32, u64, i64, P, P, P]
     L.come_walks_reference.argtypes = [P, P, i64, i32, P, P, i32, f64, P, i32, P]

@@ -690,7 +690,9 @@ struct RespDbShape {
     static_assert(IMG % 256 == 0, "an image is a whole number of 1 KiB copies");
 };
 
-template <int D>
+// VAR: the calling kernel's variant.  One instantiation per kernel: the host pass of hipcc
+// rejects a second host-side use of a device template holding global_load_lds.
+template <int D, int VAR>
 __device__ __forceinline__ void resp_db_stage(const RespArgs &a, int k, float *buf, int wid,
                                               int lane) {
     using RS = RespDbShape<D>;
@@ -715,8 +717,67 @@ __device__ __forceinline__ void resp_db_stage(const RespArgs &a, int k, float *b
     }
 }
 
-template <int D>
+// One component's epilogue for a wavefront's 32 x D tile in acc (acc[ct][e] = y - mu_k P_k when
+// FOLD, else y, with mpv[ct] = (mu_k P_k)[ct * 32 + r] subtracted here): the sum of squares over the
+// row, the reduce-scatter over the 32 columns of a half-wave (as k_gmm_resp_mfma), the
+// log-probability store and the online log-sum-exp update.
+template <int D, bool FOLD>
+__device__ __forceinline__ void resp_db_epilogue(
+    const __attribute__((ext_vector_type(16))) float (&acc)[D / 32], const float (&mpv)[D / 32],
+    float lnk, int k, int r, int64_t my_row, const RespArgs &a, float &run_max, float &run_sum) {
+    constexpr int CT = D / 32;
+    float sq[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        sq[e] = 0.0f;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const float y = FOLD ? acc[ct][e] : acc[ct][e] - mpv[ct];
+            sq[e] = __builtin_fmaf(y, y, sq[e]);
+        }
+    }
+    const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
+    auto scatter_stage = [](float *v, int n, int keep_hi, auto partner) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const float keep = keep_hi ? v[i + n] : v[i];
+            const float send = keep_hi ? v[i] : v[i + n];
+            v[i] = keep + partner(send);
+        }
+    };
+    auto dpp = [](float x, auto ctrl) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
+                                                          decltype(ctrl)::value, 0xF, 0xF,
+                                                          false));
+    };
+    scatter_stage(sq, 8, b3, [&](float x) { return dpp(x, std::integral_constant<int, 0x140>{}); });
+    scatter_stage(sq, 4, b2, [&](float x) { return dpp(x, std::integral_constant<int, 0x141>{}); });
+    scatter_stage(sq, 2, b0, [&](float x) { return dpp(x, std::integral_constant<int, 0xB1>{}); });
+    scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
+    const float tot = reduce_stage<4>(sq[0]);  // + the other 16 columns (lane r ^ 16)
+    const float lp = lnk - 0.5f * tot;
+    if (r < 16 && my_row < a.V) a.resp[my_row * a.K + k] = lp;
+    if (lp > run_max) {  // online log-sum-exp of the row's components so far
+        run_sum = run_sum * expf(run_max - lp) + 1.0f;
+        run_max = lp;
+    } else {
+        run_sum += expf(lp - run_max);
+    }
+}
+
+// VAR 1: plain; VAR 2: STAG; VAR 3: STAG + FOLD.
+// STAG: waves 4-7 (the second wave of each SIMD) run each component's epilogue one component
+// late -- at the head of the next component, before its MFMAs -- so on every SIMD one wave's VALU
+// epilogue sits beside its partner's MFMAs instead of both waves reaching it together
+// (MI355X_MICROARCH.md, two waves per SIMD, item 9).  The late waves keep the tile's acc across
+// the barrier and (mu_k P_k, log_norm_k) in registers, since that LDS buffer is re-staged.
+// Outputs are bit-identical to STAG = false.
+// FOLD: the accumulators start at -(mu_k P_k) instead of 0, so the MFMA chain itself forms
+// y - mu_k P_k (64 fewer VALU per component and wavefront; a different fp32 rounding than
+// k_gmm_resp_mfma's, checked against float64).
+template <int D, int VAR>
 __global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
+    constexpr bool STAG = VAR >= 2, FOLD = VAR >= 3;
     using RS = RespDbShape<D>;
     constexpr int CT = D / 32;
     constexpr int G = D / 8;
@@ -726,6 +787,7 @@ __global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
+    const bool late = STAG && wid >= 4;
     const int64_t blk0 = (int64_t)blockIdx.x * (32 * RS::WAVES);
     const int64_t myrow = blk0 + wid * 32 + r;
     const bool rowok = myrow < a.V;
@@ -735,22 +797,29 @@ __global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
         xa[g] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         if (rowok) xa[g] = *reinterpret_cast<const f32x4 *>(a.x + myrow * D + 8 * g + 4 * h);
     }
-    resp_db_stage<D>(a, 0, sm, wid, lane);
+    resp_db_stage<D, VAR>(a, 0, sm, wid, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int my_e = 8 * ((r >> 3) & 1) + 4 * ((r >> 2) & 1) + 2 * (r & 1) + ((r >> 1) & 1);
     const int64_t my_row = blk0 + wid * 32 + (my_e & 3) + 8 * (my_e >> 2) + 4 * h;
     float run_max = -INFINITY, run_sum = 0.0f;
+    f32x16 acc[CT];
+    float mpv[CT];
+    float lnk_prev = 0.0f;
     for (int k = 0; k < a.K; ++k) {
         const float *buf = sm + (k & 1) * RS::BUF;
-        if (k + 1 < a.K) resp_db_stage<D>(a, k + 1, sm + ((k + 1) & 1) * RS::BUF, wid, lane);
+        if (k + 1 < a.K) resp_db_stage<D, VAR>(a, k + 1, sm + ((k + 1) & 1) * RS::BUF, wid, lane);
         const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(buf[RS::PAR])) != 0;
         const float lnk = buf[RS::PAR + 1];
-        f32x16 acc[CT];
+        if (late && k > 0)
+            resp_db_epilogue<D, FOLD>(acc, mpv, lnk_prev, k - 1, r, my_row, a, run_max, run_sum);
+        const float *mps = buf + RS::MP;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) mpv[ct] = mps[ct * 32 + r];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
+            for (int e = 0; e < 16; ++e) acc[ct][e] = FOLD ? -mpv[ct] : 0.0f;
         {
             auto fetch = [&](int g, f32x4 (&bv)[CT]) {
 #pragma unroll
@@ -774,50 +843,13 @@ __global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
                     }
             }
         }
-        const float *mps = buf + RS::MP;
-        float sq[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            sq[e] = 0.0f;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const float y = acc[ct][e] - mps[ct * 32 + r];
-                sq[e] = __builtin_fmaf(y, y, sq[e]);
-            }
-        }
-        // reduce-scatter over the 32 columns of a half-wave (as k_gmm_resp_mfma)
-        const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
-        auto scatter_stage = [](float *v, int n, int keep_hi, auto partner) {
-#pragma unroll
-            for (int i = 0; i < n; ++i) {
-                const float keep = keep_hi ? v[i + n] : v[i];
-                const float send = keep_hi ? v[i] : v[i + n];
-                v[i] = keep + partner(send);
-            }
-        };
-        auto dpp = [](float x, auto ctrl) {
-            return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
-                                                              decltype(ctrl)::value, 0xF, 0xF,
-                                                              false));
-        };
-        scatter_stage(sq, 8, b3, [&](float x) { return dpp(x, std::integral_constant<int, 0x140>{}); });
-        scatter_stage(sq, 4, b2, [&](float x) { return dpp(x, std::integral_constant<int, 0x141>{}); });
-        scatter_stage(sq, 2, b0, [&](float x) { return dpp(x, std::integral_constant<int, 0xB1>{}); });
-        scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
-        const float tot = reduce_stage<4>(sq[0]);
-        {
-            const float lp = lnk - 0.5f * tot;
-            if (r < 16 && my_row < a.V) a.resp[my_row * a.K + k] = lp;
-            if (lp > run_max) {
-                run_sum = run_sum * expf(run_max - lp) + 1.0f;
-                run_max = lp;
-            } else {
-                run_sum += expf(lp - run_max);
-            }
-        }
+        if (!late) resp_db_epilogue<D, FOLD>(acc, mpv, lnk, k, r, my_row, a, run_max, run_sum);
+        lnk_prev = lnk;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; P_{k+1} in the other buffer
     }
+    if (late)
+        resp_db_epilogue<D, FOLD>(acc, mpv, lnk_prev, a.K - 1, r, my_row, a, run_max, run_sum);
     if (r < 16 && my_row < a.V) {
         float *lp = a.resp + my_row * a.K;
         const float lse = run_max + logf(run_sum);
@@ -1548,17 +1580,24 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         if (current_opts().gmm_resp_db) {
             const size_t lds_db = sizeof(float) * (size_t)(d == 64 ? RespDbShape<64>::LDS
                                                                     : RespDbShape<128>::LDS);
-            void (*kdb)(RespArgs) = d == 64 ? k_gmm_resp_db<64> : k_gmm_resp_db<128>;
+            // 1 = double-buffered, 2 = + staggered epilogue, 3 = + folded mu_k P_k
+            static void (*const kdbs[3][2])(RespArgs) = {
+                {k_gmm_resp_db<64, 1>, k_gmm_resp_db<128, 1>},
+                {k_gmm_resp_db<64, 2>, k_gmm_resp_db<128, 2>},
+                {k_gmm_resp_db<64, 3>, k_gmm_resp_db<128, 3>}};
+            const int var = current_opts().gmm_resp_db;
+            if (var < 1 || var > 3) return set_error(COME_E_INVALID, "gmm_resp_db must be 0..3");
             static bool attr_db = false;
             if (!attr_db) {
-                (void)hipFuncSetAttribute((const void *)k_gmm_resp_db<64>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                (void)hipFuncSetAttribute((const void *)k_gmm_resp_db<128>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                for (auto &row : kdbs)
+                    for (auto f : row)
+                        (void)hipFuncSetAttribute((const void *)f,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  160 * 1024);
                 attr_db = true;
             }
-            hipLaunchKernelGGL(kdb, dim3((unsigned)((V + 255) / 256)), dim3(512), lds_db,
-                               (hipStream_t)stream, a);
+            hipLaunchKernelGGL(kdbs[var - 1][d == 64 ? 0 : 1], dim3((unsigned)((V + 255) / 256)),
+                               dim3(512), lds_db, (hipStream_t)stream, a);
             return hip_error(hipGetLastError(), "k_gmm_resp_db launch");
         }
         const unsigned grid = (unsigned)((V + 127) / 128);

@@ -9,11 +9,15 @@ identical to the single-GPU run), and every ``sync_every`` batches the ranks exc
 changed:
 
     delta_r = W_r - W_sync          (local progress since the last sync)
-    W       = W_sync + sum_r delta_r  (all-reduce SUM over RCCL / xGMI)
+    W       = W_sync + combine_r delta_r  (all-reduce SUM over RCCL / xGMI, then the combine)
     W_sync  = W
 
-Summing deltas keeps every rank's Hogwild progress (plain averaging would shrink each rank's
-steps by 1/N).  With N = 1 sync is a no-op.  The all-reduce runs on torch.distributed with the
+Combine rules (``combine=``): "sum" (SURVEY.md §8e's first-order merge: every rank's progress
+kept), "mean" (model averaging), "touched_mean" (a row moves by the mean delta of the ranks that
+changed it -- one extra uint8 all-reduce of the per-row change flags) and "hot_mean" (given rows
+averaged, the rest summed).  The SGNS trainers default to "touched_mean": at lr 0.1 the sum
+diverges once N replicas saturate the same hub rows within a period (multi-rank tier C,
+DESIGN.md §6).  With N = 1 sync is a no-op.  The all-reduce runs on torch.distributed with the
 "nccl" backend (= RCCL on ROCm); tests run the same code on "gloo" with CPU tensors.
 
 Overlap (``start`` / ``finish``): the exchange of batch s runs on RCCL's stream while batch s+1

@@ -62,10 +62,14 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-def test_estep_mixed_factor_shapes(d):
+@pytest.mark.parametrize("variant", [0, 3])
+def test_estep_mixed_factor_shapes(d, variant):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
-    loop.  Mixed in one launch, every component must match the float64 quadratic form."""
+    loop.  Mixed in one launch, every component must match the float64 quadratic form -- for
+    k_gmm_resp_mfma (variant 0) and the staggered double-buffered kernel whose accumulators start
+    at -mu_k P_k (gmm_resp_db = 3)."""
+    from come_amd import _lib
     V, K = 1500, 6
     rng = np.random.RandomState(d)
     X = rng.standard_normal((V, d)).astype(np.float32)
@@ -80,7 +84,11 @@ def test_estep_mixed_factor_shapes(d):
     ln = np.log(np.full(K, 1.0 / K))
     mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
+    try:
+        _lib.set_option("gmm_resp_db", variant)
+        resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
+    finally:
+        _lib.set_option("gmm_resp_db", 0)
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
     lp = ln[None] - 0.5 * (Y ** 2).sum(-1)
     from scipy.special import logsumexp
@@ -239,9 +247,11 @@ def test_community2vec_trains_at_d256():
                                    (257, 1, 128)])
 def test_estep_double_buffered_kernel_bit_identical(V, K, d):
     """k_gmm_resp_db (gmm_resp_db=1: one 8-wavefront workgroup per CU, P_{k+1} staged into the
-    second LDS buffer while component k computes) against k_gmm_resp_mfma: the same MFMA order per
-    column tile and the same epilogue -> bit-identical responsibilities and log-sum-exp, with
-    upper, lower and dense factors mixed and ragged row counts."""
+    second LDS buffer while component k computes; =2: the second wave of each SIMD runs every
+    epilogue one component late) against k_gmm_resp_mfma: the same MFMA order per column tile and
+    the same epilogue -> bit-identical responsibilities and log-sum-exp, with upper, lower and
+    dense factors mixed and ragged row counts.  =3 (accumulators start at -mu_k P_k) rounds
+    differently: checked to float tolerance against the others."""
     from come_amd import _lib
     rng = np.random.RandomState(V + K + d)
     X = rng.standard_normal((V, d)).astype(np.float32)
@@ -256,11 +266,14 @@ def test_estep_double_buffered_kernel_bit_identical(V, K, d):
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev())  # noqa: E731
     out = []
     try:
-        for opt in (0, 1):
+        for opt in (0, 1, 2, 3):
             _lib.set_option("gmm_resp_db", opt)
             r, l = gmm.estep(t(X), t(P), t(mp), t(ln))
             out.append((r.cpu().numpy(), l.cpu().numpy()))
     finally:
         _lib.set_option("gmm_resp_db", 0)
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
+    for o in out[1:3]:
+        np.testing.assert_array_equal(out[0][0], o[0])
+        np.testing.assert_array_equal(out[0][1], o[1])
+    np.testing.assert_allclose(out[3][0], out[0][0], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(out[3][1], out[0][1], rtol=1e-5, atol=1e-4)
