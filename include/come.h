@@ -260,6 +260,9 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       with the second wave of each SIMD one epilogue late (both bit-identical
  *                       to 0); 3 = 2 with the accumulators started at -mu_k P_k (own rounding);
  *                       other values: COME_E_INVALID at the call
+ *   gmm_resp16          GMM E-step at d = 64, 128 on 16x16x4 MFMAs (k_gmm_resp16: 16-wide
+ *                       triangular skip, balanced half images, in-lane row sums); takes
+ *                       precedence over gmm_resp_db
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM
@@ -280,6 +283,7 @@ typedef struct come_launch_opts {
     int o2_fresh_loads;
     int o2_atomic_writeback;
     int gmm_resp_db;
+    int gmm_resp16;
     uint64_t *o2_update_count;
 } come_launch_opts;
 

@@ -450,12 +450,15 @@ __global__ void __launch_bounds__(256, 2) k_community_async(CommArgs a) {
 // barrier is a plain __syncthreads (its vmcnt(0) retires exactly the copies the next phase reads).
 // No VGPRs are spent on staging.
 __global__ void __launch_bounds__(256) k_gmm_lower_flags(const float *__restrict__ P, int D,
-                                                         int *__restrict__ flags) {
+                                                         int *__restrict__ flags, int K) {
     const float *Pk = P + (int64_t)blockIdx.x * D * D;
     int nz = 0;
     for (int o = threadIdx.x; o < D * D; o += 256) nz |= (o / D > o % D) && Pk[o] != 0.0f;
     nz = __syncthreads_or(nz);
-    if (threadIdx.x == 0) flags[blockIdx.x] = nz ? 1 : 0;
+    if (threadIdx.x == 0) {
+        flags[blockIdx.x] = nz ? 1 : 0;
+        if (nz) atomicOr(flags + K, 1);  // flags[K]: some component is not upper-triangular
+    }
 }
 
 // Pt[k][c][s] = P[k][s][c] (one D x D matrix per blockIdx.y, 32 x 32 tiles through LDS)
@@ -856,6 +859,249 @@ __global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
         for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
         if (a.lse) a.lse[my_row] = lse;
     }
+}
+
+// ---- E-step on v_mfma_f32_16x16x4_f32 (k_gmm_resp16) -------------------------------------------
+//
+// Y^T = P_k^T X^T per 16 x 16 tile: A = P_k^T (lane: column c = ct*16 + lane%16, features
+// 16q + 4 (lane/16) + t), B = X^T (lane: row = rt*16 + lane%16, the same features), so the four
+// k-slots of an MFMA step t are features 16q + {0, 4, 8, 12} + t and each lane's A operands for
+// the four steps of quad q are ONE ds_read_b128 (its B operands one f32x4 register).  The output
+// lane holds column 4 (lane/16) + e of row lane%16, so a row's sum of squares is the lane's own
+// 4 x CT values plus two cross-lane adds (lane ^ 16, lane ^ 32) -- no reduce-scatter.
+// 16-wide blocks skip more of sklearn's upper precision factor than 32-wide ones: block (quad q,
+// column tile ct) is non-zero iff q <= ct, 36 of 64 blocks at d = 128 (0.5625 of the dense MFMA
+// cycles; k_gmm_resp_mfma: 10 of 16 32-wide blocks = 0.625), at the same fp32 rate (32 cycles per
+// 16x16x4 MFMA = 64 per 32x32x2, half the flops).
+// A workgroup = 4 wavefronts x 32 rows (RT = 2 row tiles), two workgroups per CU.  P_k^T lives in
+// LDS as two half images of D rows x D/2 features; half 0 holds quads {0 .. NQ/4-1} and
+// {3NQ/4 .. NQ-1}, half 1 the middle ones, so both phases of a component run the same number of
+// MFMAs (18 + 18 (quad, tile) blocks at d = 128; k_gmm_resp_mfma's halves: 112 vs 48 MFMAs).
+// The next component's half is copied global -> LDS (global_load_lds) while the other half
+// computes, as in k_gmm_resp_mfma.  Rows of an image are 16-B granules XOR-swizzled by the row
+// (granule g of row r at g ^ (r % granules)): conflict-free ds_read_b128 without padding.
+template <int D>
+struct Resp16Shape {
+    static constexpr int NQ = D / 16;        // feature quads = column tiles
+    static constexpr int HQ = NQ / 2;        // quads per half image
+    static constexpr int GR = HQ * 4;        // 16-B granules per half-image row
+    static constexpr int HIMG = D * GR * 4;  // floats per half image
+    static constexpr int MP = 2 * HIMG;      // mu_k P_k (D floats, 256 reserved)
+    static constexpr int PARAMS = MP + 256;  // lower flag, log_norm (64 reserved)
+    static constexpr int LDS = PARAMS + 64;  // floats
+    static_assert(HIMG % 256 == 0, "a half image is a whole number of 1 KiB copies");
+};
+
+// the quad held at position p of half image h
+template <int D>
+__host__ __device__ constexpr int r16_quad(int h, int p) {
+    return h == 0 ? (p < D / 64 ? p : p + D / 32) : p + D / 64;
+}
+
+// Per-lane source offsets (floats, within one D x D matrix) of the 1 KiB pieces wavefront `wid`
+// copies for half image h: piece i = wid + 4 j holds granules 64 i .. 64 i + 63 of the image.
+template <int D>
+struct R16Stage {
+    static constexpr int PIECES = Resp16Shape<D>::HIMG / 256;
+    static constexpr int PER_WAVE = (PIECES + 3) / 4;
+    uint32_t off[2][PER_WAVE];  // bytes: a 32-bit vector offset from a scalar base
+    __device__ __forceinline__ R16Stage(int wid, int lane) {
+        using RS = Resp16Shape<D>;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < PER_WAVE; ++j) {
+                const int g = (wid + 4 * j) * 64 + lane;
+                const int r = g / RS::GR, logical = (g % RS::GR) ^ (r & (RS::GR - 1));
+                off[h][j] = 4u * (uint32_t)(r * D + 16 * r16_quad<D>(h, logical >> 2) +
+                                            4 * (logical & 3));
+            }
+    }
+    // copy half image h of P_k^T (4 wavefronts, 1 KiB per instruction)
+    __device__ __forceinline__ void half(const float *Ptk, float *sm, int h, int wid) const {
+#pragma unroll
+        for (int j = 0; j < PER_WAVE; ++j) {
+            const int i = wid + 4 * j;
+            if (i >= PIECES) break;  // wavefront-uniform
+            __builtin_amdgcn_global_load_lds(
+                reinterpret_cast<const float *>(reinterpret_cast<const char *>(Ptk) + off[h][j]),
+                sm + h * Resp16Shape<D>::HIMG + i * 256, 16, 0, 0);
+        }
+    }
+};
+
+// F: the calling body's FULL (one instantiation per body: the host pass of hipcc rejects a
+// second host-side use of a device template holding global_load_lds)
+template <int D, bool F>
+__device__ __forceinline__ void r16_stage_mp(const float *mp, float *sm, int wid, int lane) {
+    if (wid == 0) {
+        const int src = lane * 4 < D ? lane * 4 : D - 4;
+        __builtin_amdgcn_global_load_lds(mp + src, sm + Resp16Shape<D>::MP, 16, 0, 0);
+    }
+}
+
+template <int D, bool F>
+__device__ __forceinline__ void r16_stage_params(const RespArgs &a, int k, float *sm, int wid,
+                                                 int lane) {
+    if (wid == 0) {
+        const float *src = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
+                                     : a.log_norm + k;
+        __builtin_amdgcn_global_load_lds(src, sm + Resp16Shape<D>::PARAMS, 4, 0, 0);
+    }
+}
+
+// Blocks (position p in half image H, column tile ct) of one phase in issue order: every tile
+// of a quad (FULL: a lower or dense factor) or only ct >= q (upper factor).
+template <int D>
+constexpr int r16_nblk(int H, bool full) {
+    int n = 0;
+    for (int p = 0; p < D / 32; ++p) n += full ? D / 16 : D / 16 - r16_quad<D>(H, p);
+    return n;
+}
+template <int D>
+constexpr int r16_blk(int H, bool full, int n, bool want_ct) {
+    for (int p = 0; p < D / 32; ++p)
+        for (int ct = full ? 0 : r16_quad<D>(H, p); ct < D / 16; ++ct)
+            if (n-- == 0) return want_ct ? ct : p;
+    return 0;
+}
+
+// One phase: the blocks of half image H on both row tiles.  Per block one ds_read_b128 of A
+// operands (four k-steps) feeds 8 MFMAs (4 steps x 2 row tiles, two independent accumulation
+// chains); A operands are read two blocks ahead (a 3-slot ring: few VGPRs).
+// abase[p] = the lane's offset (floats) of its A operands for position p in an image's first
+// column tile; tile ct adds ct * 16 rows (a compile-time immediate: the XOR swizzle depends on
+// the row only through row % granules = j16 % granules).
+template <int D, bool FULL, int H>
+__device__ __forceinline__ void r16_phase(
+    const __attribute__((ext_vector_type(4))) float (&xb)[2][D / 16], const float *sm,
+    const int (&abase)[D / 32], __attribute__((ext_vector_type(4))) float (&acc)[2][D / 16]) {
+    using RS = Resp16Shape<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int NB = r16_nblk<D>(H, FULL);
+    const float *img = sm + H * RS::HIMG;
+    auto fetch = [&](int n) {
+        const int p = r16_blk<D>(H, FULL, n, false), ct = r16_blk<D>(H, FULL, n, true);
+        return *reinterpret_cast<const f32x4 *>(img + abase[p] + ct * 16 * (RS::GR * 4));
+    };
+    f32x4 av[3];
+    av[0] = fetch(0);
+    if (NB > 1) av[1] = fetch(1);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+        if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
+        const int ct = r16_blk<D>(H, FULL, n, true);
+        const int q = r16_quad<D>(H, r16_blk<D>(H, FULL, n, false));
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[rt][q][t],
+                                                                   acc[rt][ct], 0, 0, 0);
+        // keep the ring: no A read hoisted above its block (the scheduler would otherwise
+        // cluster every read of the phase at its head and spill)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// FULL: every component runs every (quad, tile) block -- the launch holds some lower or dense
+// factor (flags[K], k_gmm_lower_flags); else the upper-triangular skip for all components.
+template <int D, bool FULL>
+__device__ __forceinline__ void r16_body(const RespArgs &a, float *sm) {
+    using RS = Resp16Shape<D>;
+    constexpr int NQ = RS::NQ;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int j16 = lane & 15, kg = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * 128 + wid * 32;
+    f32x4 xb[2][NQ];  // xb[rt][q][t] = x[row0 + 16 rt + j16][16 q + 4 kg + t]
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int64_t row = row0 + 16 * rt + j16;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            xb[rt][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (row < a.V) xb[rt][q] = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg);
+        }
+    }
+    const R16Stage<D> stage(wid, lane);
+    stage.half(a.prec_t, sm, 0, wid);
+    stage.half(a.prec_t, sm, 1, wid);
+    r16_stage_mp<D, FULL>(a.mu_prec, sm, wid, lane);
+    r16_stage_params<D, FULL>(a, 0, sm, wid, lane);
+    int abase[RS::HQ];
+#pragma unroll
+    for (int p = 0; p < RS::HQ; ++p)
+        abase[p] = j16 * (RS::GR * 4) + 4 * ((4 * p + kg) ^ (j16 & (RS::GR - 1)));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // lanes 0-15 own row tile 0, lanes 16-31 row tile 1 (the others hold copies)
+    const int64_t my_row = row0 + 16 * (kg & 1) + j16;
+    const bool owner = kg < 2 && my_row < a.V;
+    float run_max = -INFINITY, run_sum = 0.0f;
+    for (int k = 0; k < a.K; ++k) {
+        const float lnk = sm[RS::PARAMS + 1];
+        const float *Pn = a.prec_t + (int64_t)(k + 1) * D * D;
+        f32x4 acc[2][NQ];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        r16_phase<D, FULL, 0>(xb, sm, abase, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // half 0 and the params free; half 1 and mu_k P_k in LDS
+        if (k + 1 < a.K) {
+            stage.half(Pn, sm, 0, wid);
+            r16_stage_params<D, FULL>(a, k + 1, sm, wid, lane);
+        }
+        r16_phase<D, FULL, 1>(xb, sm, abase, acc);
+        float sq[2] = {0.0f, 0.0f};
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) {
+            const f32x4 mp = *reinterpret_cast<const f32x4 *>(sm + RS::MP + ct * 16 + 4 * kg);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float y = acc[rt][ct][e] - mp[e];
+                    sq[rt] = __builtin_fmaf(y, y, sq[rt]);
+                }
+        }
+        // each row's columns are spread over the 4 lane groups: sum them for both row tiles
+        const float tot0 = reduce_stage<5>(reduce_stage<4>(sq[0]));
+        const float tot1 = reduce_stage<5>(reduce_stage<4>(sq[1]));
+        const float tot = (kg & 1) ? tot1 : tot0;
+        const float lp = lnk - 0.5f * tot;
+        if (owner) a.resp[my_row * a.K + k] = lp;
+        if (lp > run_max) {  // online log-sum-exp of the row's components so far
+            run_sum = run_sum * expf(run_max - lp) + 1.0f;
+            run_max = lp;
+        } else {
+            run_sum += expf(lp - run_max);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // half 1 and mu_k P_k free; half 0 of P_{k+1} in LDS
+        if (k + 1 < a.K) {
+            stage.half(Pn, sm, 1, wid);
+            r16_stage_mp<D, FULL>(a.mu_prec + (int64_t)(k + 1) * D, sm, wid, lane);
+        }
+    }
+    if (owner) {
+        float *lp = a.resp + my_row * a.K;
+        const float lse = run_max + logf(run_sum);
+        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+        if (a.lse) a.lse[my_row] = lse;
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2) k_gmm_resp16(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0)
+        r16_body<D, true>(a, sm);
+    else
+        r16_body<D, false>(a, sm);
 }
 
 // ---- GMM M-step scatter matrices -------------------------------------------------------------
@@ -1563,10 +1809,13 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
     if (rc) return rc;
     RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K, nullptr};
     if (mfma) {
-        int *flags = (int *)stream_scratch(dev, stream, kScratchGmmFlags, sizeof(int) * K);
+        int *flags = (int *)stream_scratch(dev, stream, kScratchGmmFlags, sizeof(int) * (K + 1));
         if (!flags) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+        rc = hip_error(hipMemsetAsync(flags + K, 0, sizeof(int), (hipStream_t)stream),
+                       "gmm_resp: flag reset");
+        if (rc) return rc;
         hipLaunchKernelGGL(k_gmm_lower_flags, dim3(K), dim3(256), 0, (hipStream_t)stream,
-                           prec_chol, d, flags);
+                           prec_chol, d, flags, K);
         rc = hip_error(hipGetLastError(), "k_gmm_lower_flags launch");
         if (rc) return rc;
         a.lower = flags;
@@ -1577,6 +1826,22 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         rc = hip_error(hipGetLastError(), "k_transpose_sq launch");
         if (rc) return rc;
         a.prec_t = pt;
+        if (current_opts().gmm_resp16) {
+            const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
+                                                                   : Resp16Shape<128>::LDS);
+            void (*k16)(RespArgs) = d == 64 ? k_gmm_resp16<64> : k_gmm_resp16<128>;
+            static bool attr16 = false;
+            if (!attr16) {
+                (void)hipFuncSetAttribute((const void *)k_gmm_resp16<64>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute((const void *)k_gmm_resp16<128>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr16 = true;
+            }
+            hipLaunchKernelGGL(k16, dim3((unsigned)((V + 127) / 128)), dim3(256), lds16,
+                               (hipStream_t)stream, a);
+            return hip_error(hipGetLastError(), "k_gmm_resp16 launch");
+        }
         if (current_opts().gmm_resp_db) {
             const size_t lds_db = sizeof(float) * (size_t)(d == 64 ? RespDbShape<64>::LDS
                                                                     : RespDbShape<128>::LDS);

@@ -151,7 +151,7 @@ extern "C" int come_set_option(const char *name, int value) {
                   COME_OPT(resident_cap),     COME_OPT(community_async),
                   COME_OPT(gmm_cov_async),    COME_OPT(walk_staged),
                   COME_OPT(o2_fresh_loads),   COME_OPT(o2_atomic_writeback),
-                  COME_OPT(gmm_resp_db)};
+                  COME_OPT(gmm_resp_db),      COME_OPT(gmm_resp16)};
 #undef COME_OPT
     for (const auto &f : fields)
         if (!strcmp(f.k, name)) {

@@ -62,13 +62,14 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", [0, 3, "16"])
 def test_estep_mixed_factor_shapes(d, variant):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
     loop.  Mixed in one launch, every component must match the float64 quadratic form -- for
-    k_gmm_resp_mfma (variant 0) and the staggered double-buffered kernel whose accumulators start
-    at -mu_k P_k (gmm_resp_db = 3)."""
+    k_gmm_resp_mfma (variant 0), the staggered double-buffered kernel whose accumulators start
+    at -mu_k P_k (gmm_resp_db = 3) and the 16x16x4 kernel k_gmm_resp16 (gmm_resp16 = 1; a lower
+    or dense factor in the launch makes it run every block of every component)."""
     from come_amd import _lib
     V, K = 1500, 6
     rng = np.random.RandomState(d)
@@ -84,11 +85,12 @@ def test_estep_mixed_factor_shapes(d, variant):
     ln = np.log(np.full(K, 1.0 / K))
     mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
+    opt = ("gmm_resp16", 1) if variant == "16" else ("gmm_resp_db", variant)
     try:
-        _lib.set_option("gmm_resp_db", variant)
+        _lib.set_option(*opt)
         resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
     finally:
-        _lib.set_option("gmm_resp_db", 0)
+        _lib.set_option(opt[0], 0)
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
     lp = ln[None] - 0.5 * (Y ** 2).sum(-1)
     from scipy.special import logsumexp
@@ -277,3 +279,31 @@ def test_estep_double_buffered_kernel_bit_identical(V, K, d):
         np.testing.assert_array_equal(out[0][1], o[1])
     np.testing.assert_allclose(out[3][0], out[0][0], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(out[3][1], out[0][1], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (1000, 5, 128), (2049, 9, 64), (300, 3, 64),
+                                   (129, 1, 128)])
+def test_estep16_upper_factors_vs_float64(V, K, d):
+    """k_gmm_resp16 with sklearn-shaped (upper-triangular) precision factors only -- the launch
+    that takes the 16-wide triangular skip -- against the float64 quadratic form, ragged rows."""
+    from come_amd import _lib
+    from scipy.special import logsumexp
+    rng = np.random.RandomState(V + K)
+    X = rng.standard_normal((V, d)).astype(np.float32)
+    P = np.stack([np.triu(rng.standard_normal((d, d)) / np.sqrt(d)) + 2 * np.eye(d)
+                  for _ in range(K)])
+    mu = (rng.standard_normal((K, d)) * 0.3)
+    mp = np.einsum("kd,kde->ke", mu, P)
+    ln = np.log(rng.dirichlet(np.ones(K)))
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
+    try:
+        _lib.set_option("gmm_resp16", 1)
+        resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
+    finally:
+        _lib.set_option("gmm_resp16", 0)
+    Y = np.einsum("vd,kde->vke", X.astype(np.float64), P.astype(np.float32).astype(np.float64)) \
+        - mp.astype(np.float32)[None]
+    lp = ln.astype(np.float32)[None] - 0.5 * (Y ** 2).sum(-1)
+    ref_lse = logsumexp(lp, 1)
+    np.testing.assert_allclose(resp.cpu().numpy(), np.exp(lp - ref_lse[:, None]), atol=2e-4)
+    np.testing.assert_allclose(lse.cpu().numpy(), ref_lse, rtol=2e-5, atol=2e-3)
