@@ -89,7 +89,8 @@ def secondary_rows(timeout_s=150):
                    "roofline_frac": j["roofline"]["frac"], "roofline_bound": j["roofline"]["bound"],
                    "avg_kernel_ms": j["roofline"]["avg_kernel_ms"], "wall_s": time.time() - t0}
             if wl == "c4":
-                for k in ("gmm_resp_ms", "gmm_resp_tflops_executed", "gmm_scatter_ms",
+                for k in ("gmm_resp_kernel", "gmm_resp_ms", "gmm_resp_tflops_executed",
+                          "gmm_scatter_ms",
                           "gmm_scatter_tflops_executed", "gmm_em_iteration_ms"):
                     row[k] = j["config"][k]
             out[wl] = row

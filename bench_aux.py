@@ -166,8 +166,18 @@ def c4(args):
     pc, mp, ln = ce.gmm_resp_params(w, mu.cpu().numpy().astype(np.float64),
                                     orc.precision_cholesky(cov), dev)
     flops = 2.0 * V * K * d * d
+    # fraction of the MFMA blocks executed on sklearn's upper-triangular precision factors: the
+    # E-step's 16-wide blocks (k_gmm_resp16, 36 of 64 at d = 128) or 32-wide ones
+    # (k_gmm_resp_mfma / _db, 10 of 16); the scatter's symmetric 32-wide tiles (10 of 16)
+    from come_amd import _lib
+    opts = _lib.launch_opts()
     ct = d // 32 if d in (64, 128) else 0
-    tri = (ct * (ct + 1) / 2) / (ct * ct) if ct else 1.0  # fraction of MFMA blocks executed
+    tri = (ct * (ct + 1) / 2) / (ct * ct) if ct else 1.0
+    ct16 = d // 16 if d in (64, 128) else 0
+    tri_resp = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_resp16 else tri) if ct16 \
+        else 1.0
+    resp_kernel = ("k_gmm_resp16" if opts.gmm_resp16 else "k_gmm_resp_db" if opts.gmm_resp_db
+                   else "k_gmm_resp_mfma") if ct16 else "VALU"
     x0 = x.clone()
     xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]
 
@@ -251,9 +261,10 @@ def c4(args):
         "higher_is_better": True, "dtype": "f32", "data": "synthetic N(0,1) rows, random SPD",
         "config": {"workload": "configs[3]/C4: V=%d K=%d d=%d" % (V, K, d),
                    # E-step / scatter: 2 V K d^2 algorithmic flops, of which the kernels execute
-                   # only the upper-triangular / symmetric 32x32 blocks (10 of 16 at d = 128)
+                   # only the upper-triangular / symmetric blocks (fractions above)
+                   "gmm_resp_kernel": resp_kernel, "gmm_resp_blocks_executed": tri_resp,
                    "gmm_resp_ms": tr * 1e3, "gmm_resp_tflops_effective": flops / tr / 1e12,
-                   "gmm_resp_tflops_executed": flops * tri / tr / 1e12,
+                   "gmm_resp_tflops_executed": flops * tri_resp / tr / 1e12,
                    "gmm_scatter_ms": ts * 1e3, "gmm_scatter_tflops_effective": flops / ts / 1e12,
                    "gmm_scatter_tflops_executed": flops * tri / ts / 1e12,
                    "gmm_em_iteration_ms": te * 1e3, **dist_cfg},

@@ -255,14 +255,14 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
  *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
- *   gmm_resp_db         GMM E-step / responsibilities at d = 64, 128: 0 = k_gmm_resp_mfma;
+ *   gmm_resp_db         with gmm_resp16 = 0, the 32x32x2 E-step at d = 64, 128: 0 = k_gmm_resp_mfma;
  *                       1 = the double-buffered 8-wavefront kernel (k_gmm_resp_db); 2 = the same
  *                       with the second wave of each SIMD one epilogue late (both bit-identical
  *                       to 0); 3 = 2 with the accumulators started at -mu_k P_k (own rounding);
  *                       other values: COME_E_INVALID at the call
- *   gmm_resp16          GMM E-step at d = 64, 128 on 16x16x4 MFMAs (k_gmm_resp16: 16-wide
- *                       triangular skip, balanced half images, in-lane row sums); takes
- *                       precedence over gmm_resp_db
+ *   gmm_resp16          default 1: GMM E-step at d = 64, 128 on 16x16x4 MFMAs (k_gmm_resp16:
+ *                       16-wide triangular skip, balanced half images, in-lane row sums; 12%
+ *                       faster at C4); takes precedence over gmm_resp_db (set 0 to use that)
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM

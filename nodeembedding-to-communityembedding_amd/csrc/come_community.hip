@@ -1041,8 +1041,9 @@ __device__ __forceinline__ void r16_body(const RespArgs &a, float *sm) {
     const bool owner = kg < 2 && my_row < a.V;
     float run_max = -INFINITY, run_sum = 0.0f;
     for (int k = 0; k < a.K; ++k) {
+        const int kn = k + 1;
         const float lnk = sm[RS::PARAMS + 1];
-        const float *Pn = a.prec_t + (int64_t)(k + 1) * D * D;
+        const float *Pn = a.prec_t + (int64_t)kn * D * D;
         f32x4 acc[2][NQ];
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -1053,7 +1054,7 @@ __device__ __forceinline__ void r16_body(const RespArgs &a, float *sm) {
         __syncthreads();  // half 0 and the params free; half 1 and mu_k P_k in LDS
         if (k + 1 < a.K) {
             stage.half(Pn, sm, 0, wid);
-            r16_stage_params<D, FULL>(a, k + 1, sm, wid, lane);
+            r16_stage_params<D, FULL>(a, kn, sm, wid, lane);
         }
         r16_phase<D, FULL, 1>(xb, sm, abase, acc);
         float sq[2] = {0.0f, 0.0f};
@@ -1084,7 +1085,7 @@ __device__ __forceinline__ void r16_body(const RespArgs &a, float *sm) {
         __syncthreads();  // half 1 and mu_k P_k free; half 0 of P_{k+1} in LDS
         if (k + 1 < a.K) {
             stage.half(Pn, sm, 1, wid);
-            r16_stage_mp<D, FULL>(a.mu_prec + (int64_t)(k + 1) * D, sm, wid, lane);
+            r16_stage_mp<D, FULL>(a.mu_prec + (int64_t)kn * D, sm, wid, lane);
         }
     }
     if (owner) {

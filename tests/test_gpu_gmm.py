@@ -85,12 +85,13 @@ def test_estep_mixed_factor_shapes(d, variant):
     ln = np.log(np.full(K, 1.0 / K))
     mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    opt = ("gmm_resp16", 1) if variant == "16" else ("gmm_resp_db", variant)
     try:
-        _lib.set_option(*opt)
+        _lib.set_option("gmm_resp16", 1 if variant == "16" else 0)
+        _lib.set_option("gmm_resp_db", 0 if variant == "16" else variant)
         resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
     finally:
-        _lib.set_option(opt[0], 0)
+        _lib.set_option("gmm_resp_db", 0)
+        _lib.set_option("gmm_resp16", 1)
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
     lp = ln[None] - 0.5 * (Y ** 2).sum(-1)
     from scipy.special import logsumexp
@@ -268,12 +269,14 @@ def test_estep_double_buffered_kernel_bit_identical(V, K, d):
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev())  # noqa: E731
     out = []
     try:
+        _lib.set_option("gmm_resp16", 0)
         for opt in (0, 1, 2, 3):
             _lib.set_option("gmm_resp_db", opt)
             r, l = gmm.estep(t(X), t(P), t(mp), t(ln))
             out.append((r.cpu().numpy(), l.cpu().numpy()))
     finally:
         _lib.set_option("gmm_resp_db", 0)
+        _lib.set_option("gmm_resp16", 1)
     for o in out[1:3]:
         np.testing.assert_array_equal(out[0][0], o[0])
         np.testing.assert_array_equal(out[0][1], o[1])
@@ -296,11 +299,7 @@ def test_estep16_upper_factors_vs_float64(V, K, d):
     mp = np.einsum("kd,kde->ke", mu, P)
     ln = np.log(rng.dirichlet(np.ones(K)))
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    try:
-        _lib.set_option("gmm_resp16", 1)
-        resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
-    finally:
-        _lib.set_option("gmm_resp16", 0)
+    resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))  # the default: gmm_resp16 = 1
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P.astype(np.float32).astype(np.float64)) \
         - mp.astype(np.float32)[None]
     lp = ln.astype(np.float32)[None] - 0.5 * (Y ** 2).sum(-1)
