@@ -813,9 +813,11 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
 // Latency hiding as in the ring kernel, one pair ahead: the next pair's input row, its positive
 // (when the center changes or is hot), its negative rows and the hot bits of its rows are in
 // flight while the current pair computes; the next 64 table draws (with their hot bits) while the
-// current 64 are consumed.  A prefetched copy of a row the current pair then updates receives
-// that update additively (copy + delta), so it keeps both the other wavefronts' updates it was
-// loaded with and this wavefront's own.
+// current 64 are consumed.  A prefetched copy of a row the current pair then updates is patched:
+// a hot row's copy receives this wavefront's change additively (copy + delta: it keeps the other
+// wavefronts' atomics it was loaded with), a cold row's copy is replaced by the stored value (what
+// a read after the store returns; on walks that share no row the launch is bit-identical to the
+// sequential order, tests/test_gpu_stream.py).
 // Wavefronts per SIMD the stream kernel is compiled for: the kernel is latency-bound (one pair of
 // loads in flight per wavefront), so at d <= 128, n <= 5 it is held to 64 VGPRs for 8 waves per
 // SIMD (a 32-byte spill): 108 vs 119 ms per C3 launch at the 7 waves 70 VGPRs would give

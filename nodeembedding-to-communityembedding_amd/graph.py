@@ -15,16 +15,10 @@ import numpy as np
 
 
 class CSRGraph(object):
-    """Undirected simple graph in CSR form over rows 0..V-1 (node id = row + 1).  ``device``
-    (a torch CUDA device) runs the sort / unique passes there -- integer operations with the same
-    (stable, sorted) semantics, so the graph is identical to the numpy construction, in seconds
-    instead of minutes at 100M edges."""
+    """Undirected simple graph in CSR form over rows 0..V-1 (node id = row + 1)."""
 
-    def __init__(self, V, edges_rows, device=None):
+    def __init__(self, V, edges_rows):
         self.V = int(V)
-        if device is not None:
-            self._build_torch(edges_rows, device)
-            return
         e = np.asarray(edges_rows, np.int64).reshape(-1, 2)
         e = e[e[:, 0] != e[:, 1]]
         a = np.minimum(e[:, 0], e[:, 1])
@@ -40,27 +34,39 @@ class CSRGraph(object):
         self.rowptr = np.zeros(V + 1, np.int64)
         np.cumsum(self.degree, out=self.rowptr[1:])
 
-    def _build_torch(self, edges_rows, device):
+    @classmethod
+    def from_device_pairs(cls, V, u, v):
+        """The same graph as CSRGraph(V, stack([u, v], 1)) from 1-D CUDA int64 endpoint tensors,
+        with torch's sort / unique on the device (integer operations with the same stable,
+        sorted semantics: identical output, seconds instead of minutes at 100M pairs).  Only
+        1-D tensors, and gathers in slices of 2^24 indices: on this ROCm build torch's row
+        gathers of [1e8, 2] int64 tensors (boolean mask / index_select) return wrong rows
+        silently, and fail to launch at 2^27 rows (scripts/bisect_torch_gather.py)."""
         import torch
-        V = self.V
-        e = torch.as_tensor(np.asarray(edges_rows, np.int64).reshape(-1, 2), device=device)
-        e = e[e[:, 0] != e[:, 1]]
-        a = torch.minimum(e[:, 0], e[:, 1])
-        b = torch.maximum(e[:, 0], e[:, 1])
-        del e
-        key = torch.unique(a * V + b, sorted=True)
+        g = cls.__new__(cls)
+        g.V = V = int(V)
+        a = torch.minimum(u, v)
+        b = torch.maximum(u, v)
+        key = torch.where(u == v, torch.full_like(a, -1), a * V + b)  # self-loops -> -1
+        del a, b
+        key = torch.unique(key, sorted=True)
+        if key.numel() and int(key[0]) < 0:
+            key = key[1:]
         a, b = key // V, key % V
         del key
-        self.edges = torch.stack([a, b], dim=1).cpu().numpy()
+        g.edges = torch.stack([a, b], dim=1).cpu().numpy()
         src = torch.cat([a, b])
         dst = torch.cat([b, a])
         del a, b
         order = torch.sort(src, stable=True).indices
-        self.col = dst[order].to(torch.int32).cpu().numpy()
+        step = 1 << 24
+        g.col = torch.cat([dst[order[i:i + step]] for i in range(0, order.numel(), step)]
+                          ).to(torch.int32).cpu().numpy()
         del dst, order
-        self.degree = torch.bincount(src, minlength=V).cpu().numpy().astype(np.int64)
-        self.rowptr = np.zeros(V + 1, np.int64)
-        np.cumsum(self.degree, out=self.rowptr[1:])
+        g.degree = torch.bincount(src, minlength=V).cpu().numpy().astype(np.int64)
+        g.rowptr = np.zeros(V + 1, np.int64)
+        np.cumsum(g.degree, out=g.rowptr[1:])
+        return g
 
     @property
     def num_edges(self):
@@ -107,9 +113,8 @@ def chung_lu(V, mean_degree, gamma=2.5, seed=1, device=None):
         u = torch.searchsorted(cwt, torch.as_tensor(rng.random(m), device=device), right=True)
         v = torch.searchsorted(cwt, torch.as_tensor(rng.random(m), device=device), right=True)
         perm = torch.as_tensor(rng.permutation(V), device=device)
-        e = torch.stack([perm[torch.clamp(u, max=V - 1)], perm[torch.clamp(v, max=V - 1)]], 1)
-        del u, v
-        return CSRGraph(V, e.cpu().numpy(), device=device)
+        return CSRGraph.from_device_pairs(V, perm[torch.clamp(u, max=V - 1)],
+                                          perm[torch.clamp(v, max=V - 1)])
     u = np.searchsorted(cw, rng.random(m), side="right")
     v = np.searchsorted(cw, rng.random(m), side="right")
     perm = rng.permutation(V)  # decorrelate degree from node id

@@ -221,3 +221,16 @@ def test_gmm_split_k_sums_equal_float64_reference(V, K, d):
     assert sx.dtype == torch.float64 and nk.dtype == torch.float64
     np.testing.assert_allclose(sx.numpy(), ref_sx.numpy(), rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(nk.numpy(), ref_nk.numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_chung_lu_device_path_equals_numpy():
+    """chung_lu(device=...) builds the graph with torch 1-D sort / unique / gathers
+    (CSRGraph.from_device_pairs); on any device it must equal the numpy construction exactly.
+    Run here on torch's CPU device (the GPU run of the same code: scripts/check_c5_inputs.py)."""
+    import torch
+    from come_amd.graph import chung_lu
+    for V, deg in ((3000, 8.0), (40000, 20.0)):
+        a = chung_lu(V, deg, seed=4)
+        b = chung_lu(V, deg, seed=4, device=torch.device("cpu"))
+        for n in ("edges", "col", "rowptr", "degree"):
+            np.testing.assert_array_equal(getattr(a, n), getattr(b, n), err_msg=n)
