@@ -176,8 +176,9 @@ def c4(args):
     ct16 = d // 16 if d in (64, 128) else 0
     tri_resp = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_resp16 else tri) if ct16 \
         else 1.0
-    resp_kernel = ("k_gmm_resp16" if opts.gmm_resp16 else "k_gmm_resp_db" if opts.gmm_resp_db
-                   else "k_gmm_resp_mfma") if ct16 else "VALU"
+    resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp16" if opts.gmm_resp16
+                   else "k_gmm_resp_db" if opts.gmm_resp_db else "k_gmm_resp_mfma") if ct16 \
+        else "VALU"
     x0 = x.clone()
     xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]
 

@@ -260,9 +260,13 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       with the second wave of each SIMD one epilogue late (both bit-identical
  *                       to 0); 3 = 2 with the accumulators started at -mu_k P_k (own rounding);
  *                       other values: COME_E_INVALID at the call
- *   gmm_resp16          default 1: GMM E-step at d = 64, 128 on 16x16x4 MFMAs (k_gmm_resp16:
- *                       16-wide triangular skip, balanced half images, in-lane row sums; 12%
- *                       faster at C4); takes precedence over gmm_resp_db (set 0 to use that)
+ *   gmm_resp16          GMM E-step at d = 64, 128 on 16x16x4 MFMAs (16-wide triangular skip,
+ *                       in-lane row sums): default 2 = k_gmm_resp16t (the factors' non-zero
+ *                       16x16 blocks packed, whole components double-buffered, one barrier per
+ *                       component; a launch holding a lower or dense factor runs every block);
+ *                       1 = k_gmm_resp16 (balanced half images, two barriers per component);
+ *                       0 = the 32x32x2 kernels of gmm_resp_db.  2 / 1 / 0: 7.13 / 7.24 / 8.25 ms
+ *                       at C4
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM

@@ -10,6 +10,8 @@
 // .py:65 takes a snapshot per iteration and every row's gradient reads only its own row), so the
 // `iters` loop runs inside the kernel on the LDS-resident tile and x is written back once.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 
@@ -101,6 +103,7 @@ struct RespArgs {
     int K;
     const int *lower;  // MFMA path: [K], 1 if prec_chol[k] has a non-zero below the diagonal
     const float *prec_t;  // MFMA path: [K][d][d] prec_chol[k] transposed (k_transpose_sq)
+    const float *prec_full;  // k_gmm_resp16t: P^T for the FULL body (prec_t = packed blocks)
 };
 
 __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
@@ -1105,6 +1108,200 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp16(RespArgs a) {
         r16_body<D, false>(a, sm);
 }
 
+// ---- k_gmm_resp16 on packed upper factors: one barrier per component ---------------------------
+//
+// When every factor of the launch is upper-triangular (sklearn's precisions_cholesky_), only the
+// 36 non-zero 16 x 16 blocks of P_k^T are kept (k_pack_upper16): per quad q the rows c >= 16 q,
+// 16 features each -- 36 KB instead of 64 KB at d = 128 -- so a workgroup double-buffers WHOLE
+// components (2 x 37.3 KB, two workgroups per CU): component k + 1 is copied global -> LDS while
+// k computes, and each component ends with ONE barrier instead of two (k_gmm_resp16's half
+// images).  The copy is a straight 1 KiB-per-instruction memcpy of the packed image (the swizzle
+// is applied by the pack kernel): granule g of row c's 16 features sits at g ^ ((c >> 1) & 2),
+// conflict-free for the A-operand ds_read_b128 (lane groups of 16 rows x one granule).
+template <int D>
+struct Resp16T {
+    static constexpr int NQ = D / 16;
+    static constexpr int TRI = 16 * 16 * NQ * (NQ + 1) / 2;  // floats of the packed blocks
+    static constexpr int MP = TRI;                            // mu_k P_k (256 reserved)
+    static constexpr int PAR = TRI + 256;                     // lower flag, log_norm (64 reserved)
+    static constexpr int BUF = TRI + 256 + 64;                // floats per buffer
+    static constexpr int LDS = 2 * BUF;
+    static constexpr int PIECES = TRI / 256;
+    static_assert(TRI % 256 == 0, "whole 1 KiB pieces");
+    // offset of quad q's first row block: 16 floats x sum_{q' < q} (D - 16 q') rows
+    static constexpr int off(int q) { return 16 * (16 * q * NQ - 8 * q * (q - 1)); }
+};
+
+// packed[k][off(q) + (c - 16q) * 16 + 4 (g ^ ((c >> 1) & 2)) + i] = P[k][16q + 4g + i][c], c >= 16q
+template <int D>
+__global__ void __launch_bounds__(256) k_pack_upper16(const float *__restrict__ P,
+                                                      float *__restrict__ packed) {
+    using T = Resp16T<D>;
+    const float *Pk = P + (int64_t)blockIdx.y * D * D;
+    float *out = packed + (int64_t)blockIdx.y * T::TRI;
+    for (int o = blockIdx.x * 256 + threadIdx.x; o < T::TRI; o += gridDim.x * 256) {
+        int q = 0;
+        while (q + 1 < T::NQ && o >= T::off(q + 1)) ++q;
+        const int rel = o - T::off(q);
+        const int c = 16 * q + rel / 16, slot = rel % 16;
+        const int g = (slot / 4) ^ ((c >> 1) & 2), i = slot % 4;
+        out[o] = Pk[(16 * q + 4 * g + i) * D + c];
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf, int wid,
+                                           int lane) {
+    using T = Resp16T<D>;
+    const float *src = a.prec_t + (int64_t)k * T::TRI;  // the packed blocks in this body
+#pragma unroll
+    for (int j = 0; j < (T::PIECES + 3) / 4; ++j) {
+        const int i = wid + 4 * j;
+        if (i >= T::PIECES) break;  // wavefront-uniform
+        __builtin_amdgcn_global_load_lds(src + i * 256 + lane * 4, buf + i * 256, 16, 0, 0);
+    }
+    if (wid == 0) {
+        const int s = lane * 4 < D ? lane * 4 : D - 4;
+        __builtin_amdgcn_global_load_lds(a.mu_prec + (int64_t)k * D + s, buf + T::MP, 16, 0, 0);
+    } else if (wid == 1) {
+        const float *p = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
+                                   : a.log_norm + k;
+        __builtin_amdgcn_global_load_lds(p, buf + T::PAR, 4, 0, 0);
+    }
+}
+
+// Block n of the upper triangle in row-major order (q, ct >= q), as compile-time tables.
+template <int NQ>
+struct TriBlocks {
+    static constexpr int NB = NQ * (NQ + 1) / 2;
+    int q[NB], ct[NB];
+    constexpr TriBlocks() : q(), ct() {
+        int n = 0;
+        for (int a = 0; a < NQ; ++a)
+            for (int b = a; b < NQ; ++b) {
+                q[n] = a;
+                ct[n] = b;
+                ++n;
+            }
+    }
+};
+
+// All 36 (d = 128) upper blocks of one component on both row tiles, in row-major order (q, ct >=
+// q); A operands read two blocks ahead through a 3-slot ring.
+template <int D>
+__device__ __forceinline__ void r16t_blocks(
+    const __attribute__((ext_vector_type(4))) float (&xb)[2][D / 16], const float *buf, int abase,
+    __attribute__((ext_vector_type(4))) float (&acc)[2][D / 16]) {
+    using T = Resp16T<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int NQ = T::NQ;
+    constexpr int NB = NQ * (NQ + 1) / 2;
+    constexpr TriBlocks<NQ> TB{};
+    auto fetch = [&](int n) {
+        return *reinterpret_cast<const f32x4 *>(buf + T::off(TB.q[n]) + (TB.ct[n] - TB.q[n]) * 256 +
+                                                abase);
+    };
+    f32x4 av[3];
+    av[0] = fetch(0);
+    av[1] = fetch(1);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+        if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
+        const int q = TB.q[n], ct = TB.ct[n];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[rt][q][t],
+                                                                   acc[rt][ct], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void r16t_body(const RespArgs &a, float *sm) {
+    using T = Resp16T<D>;
+    constexpr int NQ = T::NQ;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int j16 = lane & 15, kg = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * 128 + wid * 32;
+    f32x4 xb[2][NQ];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int64_t row = row0 + 16 * rt + j16;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            xb[rt][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (row < a.V) xb[rt][q] = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg);
+        }
+    }
+    r16t_stage<D>(a, 0, sm, wid, lane);
+    // the lane's A operands of block (q, ct): row ct*16 + j16 of quad q's row block
+    const int abase = j16 * 16 + 4 * (kg ^ ((j16 >> 1) & 2));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int64_t my_row = row0 + 16 * (kg & 1) + j16;
+    const bool owner = kg < 2 && my_row < a.V;
+    float run_max = -INFINITY, run_sum = 0.0f;
+    for (int k = 0; k < a.K; ++k) {
+        const float *buf = sm + (k & 1) * T::BUF;
+        if (k + 1 < a.K) r16t_stage<D>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
+        const float lnk = buf[T::PAR + 1];
+        f32x4 acc[2][NQ];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        r16t_blocks<D>(xb, buf, abase, acc);
+        float sq[2] = {0.0f, 0.0f};
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) {
+            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float y = acc[rt][ct][e] - mp[e];
+                    sq[rt] = __builtin_fmaf(y, y, sq[rt]);
+                }
+        }
+        const float tot0 = reduce_stage<5>(reduce_stage<4>(sq[0]));
+        const float tot1 = reduce_stage<5>(reduce_stage<4>(sq[1]));
+        const float lp = lnk - 0.5f * ((kg & 1) ? tot1 : tot0);
+        if (owner) a.resp[my_row * a.K + k] = lp;
+        if (lp > run_max) {
+            run_sum = run_sum * expf(run_max - lp) + 1.0f;
+            run_max = lp;
+        } else {
+            run_sum += expf(lp - run_max);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
+    }
+    if (owner) {
+        float *lp = a.resp + my_row * a.K;
+        const float lse = run_max + logf(run_sum);
+        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+        if (a.lse) a.lse[my_row] = lse;
+    }
+}
+
+// gmm_resp16 = 2: the packed, one-barrier form when every factor is upper-triangular (flags[K] ==
+// 0), else k_gmm_resp16's FULL body; prec_t points to the packed blocks, prec_full to P^T.
+template <int D>
+__global__ void __launch_bounds__(256, 2) k_gmm_resp16t(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0) {
+        RespArgs b = a;
+        b.prec_t = a.prec_full;
+        r16_body<D, true>(b, sm);
+    } else {
+        r16t_body<D>(a, sm);
+    }
+}
+
 // ---- GMM M-step scatter matrices -------------------------------------------------------------
 //
 // S_k = sum_i resp[i,k] (x_i - mu_k)(x_i - mu_k)^T, the numerator of sklearn's full covariance
@@ -1827,6 +2024,34 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         rc = hip_error(hipGetLastError(), "k_transpose_sq launch");
         if (rc) return rc;
         a.prec_t = pt;
+        if (current_opts().gmm_resp16 == 2) {
+            const int tri = d == 64 ? Resp16T<64>::TRI : Resp16T<128>::TRI;
+            float *packed = stream_scratch(dev, stream, kScratchGmmTri, sizeof(float) * (size_t)K * tri);
+            if (!packed) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+            hipLaunchKernelGGL(d == 64 ? k_pack_upper16<64> : k_pack_upper16<128>,
+                               dim3((unsigned)((tri + 255) / 256), K), dim3(256), 0,
+                               (hipStream_t)stream, prec_chol, packed);
+            rc = hip_error(hipGetLastError(), "k_pack_upper16 launch");
+            if (rc) return rc;
+            RespArgs b = a;
+            b.prec_full = a.prec_t;
+            b.prec_t = packed;
+            const size_t ldst = sizeof(float) * (size_t)std::max(
+                d == 64 ? Resp16T<64>::LDS : Resp16T<128>::LDS,
+                d == 64 ? Resp16Shape<64>::LDS : Resp16Shape<128>::LDS);
+            static bool attr16t = false;
+            if (!attr16t) {
+                (void)hipFuncSetAttribute((const void *)k_gmm_resp16t<64>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute((const void *)k_gmm_resp16t<128>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr16t = true;
+            }
+            hipLaunchKernelGGL(d == 64 ? k_gmm_resp16t<64> : k_gmm_resp16t<128>,
+                               dim3((unsigned)((V + 127) / 128)), dim3(256), ldst,
+                               (hipStream_t)stream, b);
+            return hip_error(hipGetLastError(), "k_gmm_resp16t launch");
+        }
         if (current_opts().gmm_resp16) {
             const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
                                                                    : Resp16Shape<128>::LDS);

@@ -117,7 +117,7 @@ static come_launch_opts g_opts = [] {
     o.o1_rows_per_wave = 12;
     o.community_async = 1;
     o.gmm_cov_async = 1;
-    o.gmm_resp16 = 1;
+    o.gmm_resp16 = 2;
     o.walk_staged = 1;
     return o;
 }();

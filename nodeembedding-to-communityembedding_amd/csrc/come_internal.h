@@ -28,7 +28,7 @@ int64_t *launch_counter(int device, void *stream);
 // device, stream and slot, grows on demand: the first call at a larger size allocates, so capture
 // a stream only after a warm-up call of the same shape).
 constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchHotCounts = 2, kScratchHotBits = 3,
-              kScratchSlots = 4;
+              kScratchGmmTri = 4, kScratchSlots = 5;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
 // The contended-row bitmap a Hogwild launch uses when the caller passes none (come_hot.hip):
 // rows holding >= max(1, floor(COME_DEFAULT_HOT_SHARE * T)) slots of `table` (plain uint32 or, with

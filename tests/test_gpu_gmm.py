@@ -21,6 +21,25 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
+class opts(object):
+    """Process-wide launch options set for a block and restored afterwards."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        from come_amd import _lib
+        cur = _lib.launch_opts()
+        self.old = {k: getattr(cur, k) for k in self.kv}
+        for k, v in self.kv.items():
+            _lib.set_option(k, v)
+
+    def __exit__(self, *exc):
+        from come_amd import _lib
+        for k, v in self.old.items():
+            _lib.set_option(k, v)
+
+
 def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -62,7 +81,7 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("variant", [0, 3, "16"])
+@pytest.mark.parametrize("variant", [0, 3, "16", "16t"])
 def test_estep_mixed_factor_shapes(d, variant):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
@@ -85,13 +104,9 @@ def test_estep_mixed_factor_shapes(d, variant):
     ln = np.log(np.full(K, 1.0 / K))
     mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    try:
-        _lib.set_option("gmm_resp16", 1 if variant == "16" else 0)
-        _lib.set_option("gmm_resp_db", 0 if variant == "16" else variant)
+    r16 = {"16": 1, "16t": 2}.get(variant, 0)
+    with opts(gmm_resp16=r16, gmm_resp_db=0 if r16 else variant):
         resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
-    finally:
-        _lib.set_option("gmm_resp_db", 0)
-        _lib.set_option("gmm_resp16", 1)
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
     lp = ln[None] - 0.5 * (Y ** 2).sum(-1)
     from scipy.special import logsumexp
@@ -268,15 +283,10 @@ def test_estep_double_buffered_kernel_bit_identical(V, K, d):
     ln = np.log(rng.dirichlet(np.ones(K))).astype(np.float32)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev())  # noqa: E731
     out = []
-    try:
-        _lib.set_option("gmm_resp16", 0)
-        for opt in (0, 1, 2, 3):
-            _lib.set_option("gmm_resp_db", opt)
+    for opt in (0, 1, 2, 3):
+        with opts(gmm_resp16=0, gmm_resp_db=opt):
             r, l = gmm.estep(t(X), t(P), t(mp), t(ln))
-            out.append((r.cpu().numpy(), l.cpu().numpy()))
-    finally:
-        _lib.set_option("gmm_resp_db", 0)
-        _lib.set_option("gmm_resp16", 1)
+        out.append((r.cpu().numpy(), l.cpu().numpy()))
     for o in out[1:3]:
         np.testing.assert_array_equal(out[0][0], o[0])
         np.testing.assert_array_equal(out[0][1], o[1])
@@ -286,9 +296,11 @@ def test_estep_double_buffered_kernel_bit_identical(V, K, d):
 
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (1000, 5, 128), (2049, 9, 64), (300, 3, 64),
                                    (129, 1, 128)])
-def test_estep16_upper_factors_vs_float64(V, K, d):
-    """k_gmm_resp16 with sklearn-shaped (upper-triangular) precision factors only -- the launch
-    that takes the 16-wide triangular skip -- against the float64 quadratic form, ragged rows."""
+@pytest.mark.parametrize("r16", [1, 2])
+def test_estep16_upper_factors_vs_float64(V, K, d, r16):
+    """k_gmm_resp16 (gmm_resp16 = 1) and its packed one-barrier form k_gmm_resp16t (= 2) with
+    sklearn-shaped (upper-triangular) precision factors only -- the launches that take the 16-wide
+    triangular skip -- against the float64 quadratic form, ragged rows."""
     from come_amd import _lib
     from scipy.special import logsumexp
     rng = np.random.RandomState(V + K)
@@ -299,7 +311,8 @@ def test_estep16_upper_factors_vs_float64(V, K, d):
     mp = np.einsum("kd,kde->ke", mu, P)
     ln = np.log(rng.dirichlet(np.ones(K)))
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))  # the default: gmm_resp16 = 1
+    with opts(gmm_resp16=r16):
+        resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P.astype(np.float32).astype(np.float64)) \
         - mp.astype(np.float32)[None]
     lp = ln.astype(np.float32)[None] - 0.5 * (Y ** 2).sum(-1)

@@ -401,6 +401,26 @@ def c3_1m():
     return fx, x, (ri, rp, rn), tsi.pack_table(tab), hot
 
 
+def test_o2_hogwild_at_the_bench_launch(c3_1m):
+    """Tier C at the bench's own launch: ONE Hogwild launch of 1,048,576 walks (8.07e8 pair
+    updates, the product's Context2Vec.batch_walks) on C3's graph, against the committed
+    sequential-oracle fixture of the same walks (tests/golden/tierc_c3_1m_seq.json, 41 minutes of
+    one core): within 1%."""
+    fx, x, (ri, rp, rn), packed, hot = c3_1m
+    node = torch.from_numpy(x.node0).to(DEV)
+    ctx = torch.zeros_like(node)
+    tsi.sgns_o2(node, ctx, dev(x.train), dev(x.seeds), 5, 5, packed, 0.1, 1.0, tsi.MODE_HOGWILD,
+                hot=hot)
+    torch.cuda.synchronize()
+    loss = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
+    del node, ctx
+    torch.cuda.empty_cache()
+    rel = (loss - fx["seq_loss"]) / fx["seq_loss"]
+    print("C3 bench launch (1,048,576 walks): held-out loss %.5f vs seq %.5f (rel %+.5f)" % (
+        loss, fx["seq_loss"], rel))
+    assert abs(rel) < 0.01, (loss, fx["seq_loss"])
+
+
 @pytest.mark.parametrize("world", [8, 4, 2])
 def test_o2_multi_rank_exchange_never_behind_sequential_oracle(c3_1m, world):
     """`world` ranks simulated on one GPU (tests/replica_sim.py: each rank its own replica and
