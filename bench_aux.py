@@ -176,6 +176,10 @@ def c4(args):
     ct16 = d // 16 if d in (64, 128) else 0
     tri_resp = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_resp16 else tri) if ct16 \
         else 1.0
+    tri_cov = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_cov_async == 3 else tri) \
+        if ct16 else 1.0
+    cov_kernel = ({3: "k_gmm_cov16", 0: "k_gmm_cov_mfma"}.get(opts.gmm_cov_async, "k_gmm_cov_async")
+                  if ct16 else "VALU")
     resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp16" if opts.gmm_resp16
                    else "k_gmm_resp_db" if opts.gmm_resp_db else "k_gmm_resp_mfma") if ct16 \
         else "VALU"
@@ -267,7 +271,8 @@ def c4(args):
                    "gmm_resp_ms": tr * 1e3, "gmm_resp_tflops_effective": flops / tr / 1e12,
                    "gmm_resp_tflops_executed": flops * tri_resp / tr / 1e12,
                    "gmm_scatter_ms": ts * 1e3, "gmm_scatter_tflops_effective": flops / ts / 1e12,
-                   "gmm_scatter_tflops_executed": flops * tri / ts / 1e12,
+                   "gmm_scatter_kernel": cov_kernel, "gmm_scatter_blocks_executed": tri_cov,
+                   "gmm_scatter_tflops_executed": flops * tri_cov / ts / 1e12,
                    "gmm_em_iteration_ms": te * 1e3, **dist_cfg},
         "roofline": {"bound": "mfma", "achieved": flops / tg / 1e12 / world,
                      "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (per GPU)",

@@ -1705,6 +1705,210 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
     }
 }
 
+// ---- M-step scatter on v_mfma_f32_16x16x4_f32 (k_gmm_cov16, gmm_cov_async = 3) ----------------
+//
+// k_gmm_cov_async's structure (4 MFMA + 4 staging wavefronts, CPW components per workgroup, two
+// image buffers, two workgroups per CU) on 16 x 16 output tiles: the symmetric output needs the
+// 36 upper tiles of 64 at d = 128 (0.5625 of the dense MFMA cycles) instead of 10 of 16 32-wide
+// tiles (0.625).  MFMA (tile rt, ct; 4 samples): A[i][k] = w_s (x_s - mu)[rt*16 + i], B[k][j] =
+// (x_s - mu)[ct*16 + j], lane l: i = j = l % 16, samples s = 16 g + 4 (l / 16) + t for the four
+// steps t of a 16-sample group g, so each operand row of a group is ONE ds_read_b128 of the
+// transposed image B[k][c][s] (rows of 32 samples, 16-byte granules XOR-swizzled by c % 8:
+// conflict-free without padding).  A d = 128 component's 36 tiles split 18 / 18 over two
+// wavefronts by tile rows {0, 1, 6, 7} and {2, 3, 4, 5}; a wavefront weights its 4 A rows once
+// per group and streams the B rows column by column (few VGPRs at 4 waves per SIMD).
+template <int D>
+struct Cov16 {
+    static constexpr int RB = 32;                 // samples per block
+    static constexpr int LDT = RB;                // image row (swizzled, unpadded)
+    static constexpr int IMG = D * LDT;
+    static constexpr int CPW = D == 128 ? 2 : 4;  // components per workgroup
+    static constexpr int WOFF = CPW * IMG;
+    static constexpr int BUF = CPW * IMG + CPW * RB;
+    static constexpr int NBUF = 2;
+    static constexpr int NT16 = D / 16;
+    static constexpr int WPC = D == 128 ? 2 : 1;  // MFMA wavefronts per component
+    static constexpr int NTW = NT16 * (NT16 + 1) / 2 / WPC;  // tiles per wavefront
+    static constexpr int NR = 4;                  // A rows per wavefront
+};
+
+// Tiles of MFMA wavefront part p (0 / 1 at d = 128; 0 at d = 64) in issue order (column-major:
+// B row ct once per column), with their A-row slot.
+template <int D>
+struct Cov16Tiles {
+    using C = Cov16<D>;
+    int rows[2][C::NR];
+    int ct[2][C::NTW], slot[2][C::NTW];
+    constexpr Cov16Tiles() : rows(), ct(), slot() {
+        for (int p = 0; p < C::WPC; ++p) {
+            for (int i = 0; i < C::NR; ++i)
+                rows[p][i] = D == 64 ? i : (p == 0 ? (i < 2 ? i : i + 4) : i + 2);
+            int n = 0;
+            for (int c = 0; c < C::NT16; ++c)
+                for (int i = 0; i < C::NR; ++i)
+                    if (rows[p][i] <= c) {
+                        ct[p][n] = c;
+                        slot[p][n] = i;
+                        ++n;
+                    }
+        }
+    }
+};
+
+template <int D>
+__device__ __forceinline__ int cov16_off(int c, int gran) {  // image offset of (row c, granule)
+    return c * Cov16<D>::LDT + 4 * (gran ^ (c & 7));
+}
+
+template <int D, int P>
+__device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, int lane,
+                                              __attribute__((ext_vector_type(4)))
+                                              float (&acc)[Cov16<D>::NTW]) {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr Cov16Tiles<D> TT{};
+    const int j16 = lane & 15, kg = lane >> 4;
+    for (int j = 0; j < nb; ++j) {
+        __syncthreads();  // barrier j: block j staged
+        const float *buf = img + (j % C::NBUF) * C::BUF;
+        const float *im = buf + tk * C::IMG;
+#pragma unroll
+        for (int g = 0; g < C::RB / 16; ++g) {
+            const int gran = 4 * g + kg;
+            const f32x4 w = *reinterpret_cast<const f32x4 *>(buf + C::WOFF + tk * C::RB + 4 * gran);
+            f32x4 wa[C::NR];
+#pragma unroll
+            for (int i = 0; i < C::NR; ++i)
+                wa[i] = w * *reinterpret_cast<const f32x4 *>(
+                                im + cov16_off<D>(TT.rows[P][i] * 16 + j16, gran));
+            f32x4 bv[2];
+            bv[0] = *reinterpret_cast<const f32x4 *>(im + cov16_off<D>(TT.ct[P][0] * 16 + j16, gran));
+            int cur = 0;
+#pragma unroll
+            for (int n = 0; n < C::NTW; ++n) {
+                // the next column's B row, read while this column's MFMAs run
+                if (n + 1 < C::NTW && TT.ct[P][n + 1] != TT.ct[P][n])
+                    bv[cur ^ 1] = *reinterpret_cast<const f32x4 *>(
+                        im + cov16_off<D>(TT.ct[P][n + 1] * 16 + j16, gran));
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[TT.slot[P][n]][t], bv[cur][t],
+                                                                  acc[n], 0, 0, 0);
+                if (n + 1 < C::NTW && TT.ct[P][n + 1] != TT.ct[P][n]) cur ^= 1;
+            }
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(CovShape<D>::ATHREADS)
+    __attribute__((amdgpu_waves_per_eu(4))) k_gmm_cov16(CovArgs a) {
+    using C = Cov16<D>;
+    constexpr int CPW = C::CPW;
+    constexpr int NST = 64 * CovShape<D>::AWAVES;  // staging threads
+    constexpr int RB = C::RB;
+    constexpr int SPT = RB * D / NST;  // samples staged per thread (16 at d = 128, 8 at d = 64)
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    static_assert(SPT % 4 == 0 && SPT * CPW <= 64 && D % 64 == 0, "staging layout");
+    static_assert(C::NBUF * C::BUF * sizeof(float) * 2 <= 160 * 1024, "two workgroups per CU");
+    __shared__ __attribute__((aligned(16))) float img[C::NBUF * C::BUF];
+    const int k0 = blockIdx.x * CPW;
+    const int nk = a.K - k0 < CPW ? a.K - k0 : CPW;
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int nb = c1 > c0 ? (int)((c1 - c0 + RB - 1) / RB) : 0;
+    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wid < CovShape<D>::AWAVES) {
+        // ---- MFMA wavefronts: component tk, tile part p ----
+        const int tk = wid / C::WPC, p = wid % C::WPC;
+        f32x4 acc[C::NTW];
+#pragma unroll
+        for (int n = 0; n < C::NTW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (nb > 0) {
+            if (p == 0) cov16_consume<D, 0>(img, nb, tk, lane, acc);
+            else cov16_consume<D, (C::WPC > 1 ? 1 : 0)>(img, nb, tk, lane, acc);
+        }
+        if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+        constexpr Cov16Tiles<D> TT{};
+        const int j16 = lane & 15, kg = lane >> 4;
+        float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
+#pragma unroll
+        for (int n = 0; n < C::NTW; ++n) {
+            const int rt = p == 0 ? TT.rows[0][TT.slot[0][n]] : TT.rows[C::WPC - 1][TT.slot[C::WPC - 1][n]];
+            const int ct = p == 0 ? TT.ct[0][n] : TT.ct[C::WPC - 1][n];
+            const int jj = ct * 16 + j16;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ii = rt * 16 + 4 * kg + e;
+                out[(int64_t)ii * D + jj] = acc[n][e];
+                if (rt != ct) out[(int64_t)jj * D + ii] = acc[n][e];
+            }
+        }
+        return;
+    }
+    // ---- staging wavefronts (as k_gmm_cov_async): thread owns column sc and samples SPT sp ..
+    // SPT sp + SPT - 1 of a block; lane l < SPT * CPW also carries one weight ----
+    const int st = tid - NST;
+    const int sc = st % D, sp = st / D;
+    float mu[CPW];
+#pragma unroll
+    for (int kk = 0; kk < CPW; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
+    float xv[3][SPT];
+    float wl[3];
+    const int wk = lane / SPT, ws = lane % SPT;
+    const bool wlane = lane < SPT * CPW;
+    auto load = [&](int blk, float (&xr)[SPT], float &wr) {
+        const int64_t b = c0 + (int64_t)blk * RB;
+        const float *src = a.x + (b + SPT * sp) * D + sc;
+        if (b + RB <= c1) {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) xr[q] = src[q * D];
+        } else {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) xr[q] = b + SPT * sp + q < c1 ? src[q * D] : 0.0f;
+        }
+        const int64_t wrow = b + SPT * sp + ws;
+        wr = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
+    };
+    auto stage = [&](int blk, const float (&xr)[SPT], float wr) {
+        float *buf = img + (blk % C::NBUF) * C::BUF;
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+            for (int j = 0; j < SPT / 4; ++j) {
+                f32x4 xb;
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) xb[q4] = xr[4 * j + q4] - mu[kk];
+                *reinterpret_cast<f32x4 *>(buf + kk * C::IMG +
+                                           cov16_off<D>(sc, (SPT * sp + 4 * j) / 4)) = xb;
+            }
+        if (wlane) buf[C::WOFF + wk * RB + SPT * sp + ws] = wr;
+    };
+    if (nb == 0) return;
+    constexpr int SD = C::NBUF - 1;  // block j + 1 is staged while block j is multiplied
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+        if (u < nb) load(u, xv[u], wl[u]);
+    if (0 < nb) {
+        stage(0, xv[0], wl[0]);
+        if (3 < nb) load(3, xv[0], wl[0]);
+    }
+    __syncthreads();  // barrier 0
+    for (int j0 = 0; j0 < nb; j0 += 3) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
+            const int j = j0 + u;
+            if (j >= nb) break;
+            if (j + SD < nb) {
+                stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+                if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+            }
+            if (j + 1 < nb) __syncthreads();  // barrier j + 1
+        }
+    }
+}
+
 // Any d <= 128 on the VALU: thread owns entries tid + 256 q of the d x d output.
 __global__ void __launch_bounds__(256) k_gmm_cov_valu(CovArgs a) {
     constexpr int MAXQ = 64;  // 128 * 128 / 256
@@ -2167,8 +2371,10 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
     const bool cov_async = current_opts().gmm_cov_async != 0;
+    const bool cov16 = mfma && current_opts().gmm_cov_async == 3;
     void (*kern)(CovArgs) =
         !mfma ? k_gmm_cov_valu
+              : cov16 ? (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>)
               : cov_async ? (current_opts().gmm_cov_async == 2
                                  ? (d == 64 ? k_gmm_cov_async<64, 3> : k_gmm_cov_async<128, 3>)
                                  : (d == 64 ? k_gmm_cov_async<64, 2> : k_gmm_cov_async<128, 2>))
@@ -2176,7 +2382,9 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const int threads = !mfma      ? 256
                         : cov_async ? CovShape<128>::ATHREADS
                                     : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
-    const int cpw = !mfma || !cov_async ? 1 : d == 64 ? CovShape<64>::CPW : CovShape<128>::CPW;
+    const int cpw = !mfma || !cov_async ? 1
+                    : cov16      ? (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW)
+                                 : (d == 64 ? CovShape<64>::CPW : CovShape<128>::CPW);
     hipLaunchKernelGGL(kern, dim3((K + cpw - 1) / cpw, used), dim3(threads), 0,
                        (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");

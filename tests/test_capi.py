@@ -64,7 +64,8 @@ def test_launch_options_snapshot_and_per_call_struct():
     ctypes LaunchOpts mirrors come_launch_opts field for field; unknown names are rejected."""
     L = _lib.lib()
     o = _lib.launch_opts()
-    assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 1
+    assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 3
+    assert o.gmm_resp16 == 2
     assert o.o2_update_count is None
     _lib.set_option("max_waves", 77)
     try:

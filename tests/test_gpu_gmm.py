@@ -118,13 +118,15 @@ def test_estep_mixed_factor_shapes(d, variant):
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
                                           (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None),
                                           (1500, 3, 256, 4), (200, 2, 330, None)])
-def test_scatter_vs_numpy(V, K, d, chunks):
+@pytest.mark.parametrize("cov", [1, 3])
+def test_scatter_vs_numpy(V, K, d, chunks, cov):
     rng = np.random.RandomState(V + K)
     X = rng.normal(size=(V, d)).astype(np.float32)
     R = rng.dirichlet(np.ones(K), V).astype(np.float32)
     M = rng.normal(size=(K, d)).astype(np.float32)
-    S = gmm.scatter(torch.as_tensor(X, device=dev()), torch.as_tensor(R, device=dev()),
-                    torch.as_tensor(M, device=dev()), chunks=chunks).cpu().numpy()
+    with opts(gmm_cov_async=cov):
+        S = gmm.scatter(torch.as_tensor(X, device=dev()), torch.as_tensor(R, device=dev()),
+                        torch.as_tensor(M, device=dev()), chunks=chunks).cpu().numpy()
     X64 = X.astype(np.float64)
     for k in range(K):
         D = X64 - M[k]
@@ -215,10 +217,11 @@ def test_community2vec_distributed_flag_single_process_matches():
                                           (5000, 3, 64, None), (65, 4, 64, 2), (700, 1, 128, 3),
                                           (517, 7, 64, 2), (1031, 9, 64, None)])
 def test_scatter_async_matches_sync(V, K, d, chunks):
-    """k_gmm_cov_async (default: 2 (d=128) / 4 (d=64) components per workgroup, operands centred
-    and weighted once per block into transposed LDS images, the same fp32 products) against the
-    synchronous k_gmm_cov_mfma: equal up to the order the MFMAs accumulate the samples in (atol
-    1e-5 of the matrix scale).  K not a multiple of the components per workgroup included."""
+    """k_gmm_cov_async (2 (d=128) / 4 (d=64) components per workgroup, operands centred and
+    weighted once per block into transposed LDS images, the same fp32 products) and k_gmm_cov16
+    (the same on 16x16x4 tiles, gmm_cov_async = 3) against the synchronous k_gmm_cov_mfma: equal
+    up to the order the MFMAs accumulate the samples in (atol 1e-5 of the matrix scale).  K not a
+    multiple of the components per workgroup included."""
     from come_amd import _lib
     rng = np.random.RandomState(V + K + d)
     t = lambda a: torch.as_tensor(a, device=dev())  # noqa: E731
@@ -226,12 +229,9 @@ def test_scatter_async_matches_sync(V, K, d, chunks):
     resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
     mu = t(rng.standard_normal((K, d)).astype(np.float32))
     out = []
-    try:
-        for opt in (0, 1, 2):  # sync; async with 2 image buffers (default) / with 3
-            _lib.set_option("gmm_cov_async", opt)
+    for opt in (0, 1, 2, 3):  # sync; async with 2 image buffers / with 3; 16x16x4 tiles
+        with opts(gmm_cov_async=opt):
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
-    finally:
-        _lib.set_option("gmm_cov_async", 1)
     for o in out[1:]:
         np.testing.assert_allclose(o, out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
 
