@@ -233,7 +233,7 @@ def main():
     # seed per walk, sharded contiguously over the ranks: rank r generates exactly its shard's
     # walks (the walker's Philox counter is the walk's global index) ----
     t0 = time.time()
-    g = chung_lu(args.nodes, args.mean_degree, gamma=2.5, seed=1)
+    g = chung_lu(args.nodes, args.mean_degree, gamma=2.5, seed=1, device=dev)  # == host build
     V, d, n, w, L = g.V, args.dim, args.negative, args.window, args.walk_length
     from come_amd.model import Model
     np.random.seed(1234)

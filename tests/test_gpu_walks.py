@@ -168,3 +168,15 @@ def test_device_walker_bit_exact_vs_cpu_restatement(alpha, L, offset):
                                walk_offset=offset, emit=em)
         np.testing.assert_array_equal(got, ref)
     assert (ref == -1).any() and (g.degree == 0).any()
+
+
+def test_chung_lu_on_the_device_equals_host_build():
+    """bench.py builds C3's graph with chung_lu(device=cuda) (torch 1-D sort / unique / gathers on
+    the GPU): it must be the host numpy construction exactly, at the bench's 1M nodes / ~10M
+    edges (C5's 10M-node graph: scripts/check_c5_inputs.py, profiles/r04k_*)."""
+    import torch
+    from come_amd.graph import chung_lu
+    a = chung_lu(1_000_000, 20.0, gamma=2.5, seed=1)
+    b = chung_lu(1_000_000, 20.0, gamma=2.5, seed=1, device=torch.device("cuda", 0))
+    for n in ("edges", "col", "rowptr", "degree"):
+        np.testing.assert_array_equal(getattr(a, n), getattr(b, n), err_msg=n)
