@@ -38,9 +38,11 @@ import numpy as np
 from . import training_sdg_inner as tsi
 from .embedding import walks_to_rows
 
-# Walks each rank trains between two exchanges in distributed mode: one full-occupancy launch
-# per rank (8,192 wavefront slots x 16); DESIGN.md §6 has the held-out loss vs period and N.
-DEFAULT_SYNC_WALKS = 1 << 17
+# Walks each rank trains between two exchanges in distributed mode (half of a batch_walks launch):
+# the held-out loss vs the sequential oracle over 4,194,304 walks is -12..-19% at 131,072 /
+# 262,144 / 524,288 walks per rank and 2-8 ranks (profiles/r04_tierc_replicas_c3_4m.json,
+# DESIGN.md §6); the longest period makes the fewest exchanges (2 per 1M-walk step).
+DEFAULT_SYNC_WALKS = 1 << 19
 
 
 def o2_pairs(rows, window):
