@@ -1062,20 +1062,42 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
                     for (int e = 0; e < VEC; ++e) dlt.v[e] = gk[k] * in.v[e];
                     dlt.atomic_add(a.ctx + (int64_t)t[k] * d, lane, d);
+                    if constexpr (VEC <= 2) {
+#pragma unroll
+                        for (int q = 1; q <= MAXN; ++q)
+                            if (tn[q] == t[k])
+#pragma unroll
+                                for (int e = 0; e < VEC; ++e) rn[q].v[e] += dlt.v[e];
+                        if (have && nci == t[k] && (npi != ic || nhi))
+#pragma unroll
+                            for (int e = 0; e < VEC; ++e) pos_n.v[e] += dlt.v[e];
+                    }
+                } else {
+                    r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
+                    if constexpr (VEC <= 2) {
+#pragma unroll
+                        for (int q = 1; q <= MAXN; ++q)
+                            if (tn[q] == t[k]) rn[q] = r[k];
+                        if (have && nci == t[k] && (npi != ic || nhi)) pos_n = r[k];
+                    }
+                }
+                if constexpr (VEC > 2) {
+                    // wide rows: one patch for hot and cold copies, the row update's own fma
+                    // (pyx:147) -- exact for a cold copy read after the previous store (it holds
+                    // the row this pair updated), and without r[k] live past its store: 149
+                    // instead of 181 VGPRs at d = 256, n = 10 (3 waves per SIMD instead of 2:
+                    // 2137 vs 2741 ms per C5 launch; at C3 the branch form above is 1.4% faster,
+                    // profiles/r04_ab_stream_patch.txt)
 #pragma unroll
                     for (int q = 1; q <= MAXN; ++q)
                         if (tn[q] == t[k])
 #pragma unroll
-                            for (int e = 0; e < VEC; ++e) rn[q].v[e] += dlt.v[e];
+                            for (int e = 0; e < VEC; ++e)
+                                rn[q].v[e] = __builtin_fmaf(gk[k], in.v[e], rn[q].v[e]);
                     if (have && nci == t[k] && (npi != ic || nhi))
 #pragma unroll
-                        for (int e = 0; e < VEC; ++e) pos_n.v[e] += dlt.v[e];
-                } else {
-                    r[k].store(a.ctx + (int64_t)t[k] * d, lane, d);
-#pragma unroll
-                    for (int q = 1; q <= MAXN; ++q)
-                        if (tn[q] == t[k]) rn[q] = r[k];
-                    if (have && nci == t[k] && (npi != ic || nhi)) pos_n = r[k];
+                        for (int e = 0; e < VEC; ++e)
+                            pos_n.v[e] = __builtin_fmaf(gk[k], in.v[e], pos_n.v[e]);
                 }
             }
             // ---- the positive: hot -> this pair's change, g * in, now (memory side) and into the
