@@ -269,6 +269,12 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       1 = k_gmm_resp16 (balanced half images, two barriers per component);
  *                       0 = the 32x32x2 kernels of gmm_resp_db.  2 / 1 / 0: 7.13 / 7.24 / 8.25 ms
  *                       at C4
+ *   o1_chunk            O1: > 0 = one wavefront per chunk of that many consecutive edges, the
+ *                       input row held in registers over each run of edges sharing it
+ *                       (k_sgns_o1_runs); default -1 = one contiguous chunk per wavefront of the
+ *                       grid (the edges in flight spread over the whole list: tier C holds in
+ *                       the reference's G.edges() order, +0.23% vs 1.6% for 0); 0 = one
+ *                       wavefront per edge (k_sgns_o1).  Sequential mode: one chunk, in order
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM
@@ -290,6 +296,7 @@ typedef struct come_launch_opts {
     int o2_atomic_writeback;
     int gmm_resp_db;
     int gmm_resp16;
+    int o1_chunk;
     uint64_t *o2_update_count;
 } come_launch_opts;
 

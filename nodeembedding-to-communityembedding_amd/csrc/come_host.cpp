@@ -118,6 +118,7 @@ static come_launch_opts g_opts = [] {
     o.community_async = 1;
     o.gmm_cov_async = 3;
     o.gmm_resp16 = 2;
+    o.o1_chunk = -1;
     o.walk_staged = 1;
     return o;
 }();
@@ -152,7 +153,8 @@ extern "C" int come_set_option(const char *name, int value) {
                   COME_OPT(resident_cap),     COME_OPT(community_async),
                   COME_OPT(gmm_cov_async),    COME_OPT(walk_staged),
                   COME_OPT(o2_fresh_loads),   COME_OPT(o2_atomic_writeback),
-                  COME_OPT(gmm_resp_db),      COME_OPT(gmm_resp16)};
+                  COME_OPT(gmm_resp_db),      COME_OPT(gmm_resp16),
+                  COME_OPT(o1_chunk)};
 #undef COME_OPT
     for (const auto &f : fields)
         if (!strcmp(f.k, name)) {

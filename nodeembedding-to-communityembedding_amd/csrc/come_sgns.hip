@@ -223,10 +223,25 @@ extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edg
         rc = derive_hot_rows(dev, table, T, packed, V, stream, &hot_rows);
         if (rc) return rc;
     }
+    const int bpc = o.o1_blocks_per_cu > 0 ? o.o1_blocks_per_cu : 6;
+    const int64_t hcap = mode == COME_MODE_HOGWILD ? hog_max_blocks(o, V, 4, o.o1_rows_per_wave) : 0;
+    int64_t chunk = o.o1_chunk;
+    if (chunk < 0) {  // auto: one contiguous chunk per wavefront of the grid
+        int dev = 0;
+        rc = ensure_init(&dev);
+        if (rc) return rc;
+        int64_t blocks = (int64_t)num_cus(dev) * bpc;
+        if (hcap > 0 && hcap < blocks) blocks = hcap;
+        const int64_t waves = mode == COME_MODE_HOGWILD ? 4 * blocks : 1;
+        chunk = (E + waves - 1) / waves;
+    }
     O1Args a{node,           edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed,
-             mode == COME_MODE_HOGWILD ? hot_rows : nullptr};
+             mode == COME_MODE_HOGWILD ? hot_rows : nullptr, chunk > 0 ? chunk : 1};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
+    if (chunk > 0)  // one wavefront per chunk of consecutive edges, the input row held
+        return launch(o, ks.o1_runs[full][maxn_index(negative)], &a, (E + chunk - 1) / chunk, mode,
+                      4, bpc, 0, stream, hcap);
     return launch(o, ks.o1[full][maxn_index(negative)], &a, E, mode, 4,
                   o.o1_blocks_per_cu > 0 ? o.o1_blocks_per_cu : 6, 0, stream,
                   mode == COME_MODE_HOGWILD ? hog_max_blocks(o, V, 4, o.o1_rows_per_wave) : 0);

@@ -1153,6 +1153,7 @@ struct O1Args {
     FastMod fm;
     int packed;
     const uint32_t *hot;  // HOG, optional: contended rows (come_hot_rows), updated atomically
+    int64_t chunk;        // k_sgns_o1_runs: consecutive edges per wavefront unit
 };
 
 template <int VEC, bool FULL, int MAXN>
@@ -1262,11 +1263,157 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
 
 // Kernel entry addresses per instantiation (defined in come_sgns_vec{1,2,4,8}.hip so the
 // instantiations compile in parallel).
+// O1 with the input row held over runs of edges (a.chunk > 0; option o1_chunk): a wavefront takes
+// `chunk` consecutive edges and processes them in order, as one of the reference's worker
+// threads does with its job of consecutive edges (node_embeddings.py:58-95).  Edge lists come
+// grouped by their first endpoint (G.edges() order: all (u, *) of a node together), so the
+// wavefront keeps node[u] in registers for the run of edges sharing u -- read once, updated by
+// every pair-1 of the run (pyx:444: input u) and read as pair 2's positive (pyx:447) -- and writes
+// it back once when u changes or the chunk ends: a float-atomic delta of the run's updates if u is
+// contended, else a plain store.  Any target row equal to the held u is taken from the registers.
+// One wavefront in sequential mode: bit-identical to k_sgns_o1 (the held row is what memory holds).
+template <int VEC, bool FULL, int MAXN>
+__global__ void __launch_bounds__(256) k_sgns_o1_runs(O1Args a) {
+    using R = Row<VEC, FULL>;
+    const int lane = threadIdx.x & 63;
+    const int64_t waves_per_block = blockDim.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * waves_per_block;
+    const LcgLane lc = lcg_lane_constants(lane);
+    const int n = a.negative;
+    const int d = a.d;
+    const int64_t nchunks = (a.E + a.chunk - 1) / a.chunk;
+
+    for (int64_t c = gw; c < nchunks; c += nwaves) {
+        const int64_t e0 = c * a.chunk;
+        const int64_t e1 = e0 + a.chunk < a.E ? e0 + a.chunk : a.E;
+        int cu = -1;        // the held row (wave-uniform), -1 = none
+        bool hot_cu = false;
+        R hu, du;           // its value and this run's change
+        auto flush = [&]() {
+            if (cu < 0) return;
+            if (hot_cu) du.atomic_add(a.node + (int64_t)cu * d, lane, d);
+            else hu.store(a.node + (int64_t)cu * d, lane, d);
+        };
+        for (int64_t e = e0; e < e1; ++e) {
+            const int u = uniform(a.edges[2 * e]);
+            const int v = uniform(a.edges[2 * e + 1]);
+            if (u < 0 || u >= a.V || v < 0 || v >= a.V) continue;  // reference: undefined
+            if (u != cu) {
+                flush();
+                cu = u;
+                hot_cu = is_hot(a, u);
+                hu.load(a.node + (int64_t)u * d, lane, d);
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) du.v[q] = 0.0f;
+            }
+            DrawBatch db;
+            db.used = 0;
+            db.base = uniform64(a.seeds[e]);
+            db.target = 0;
+            if (n > 0) draws_fill(db, db.base, lc, a, 2 * n);
+            int t1[MAXN + 1], t2[MAXN + 1];
+            bool v1[MAXN + 1], v2[MAXN + 1];
+            t1[0] = v;
+            t2[0] = u;
+            v1[0] = v2[0] = true;
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                if (k <= n) {
+                    t1[k] = (int)readlane_u32(db.target, k - 1);
+                    t2[k] = (int)readlane_u32(db.target, n + k - 1);
+                    v1[k] = t1[k] != v && t1[k] >= 0 && t1[k] < a.V;
+                    v2[k] = t2[k] != u && t2[k] >= 0 && t2[k] < a.V;
+                } else {
+                    t1[k] = t2[k] = -1;
+                    v1[k] = v2[k] = false;
+                }
+            }
+            R in2;
+            if (v != u) in2.load(a.node + (int64_t)v * d, lane, d);
+            const bool hot_v = is_hot(a, v);
+            R r1[MAXN + 1], r2[MAXN + 1];
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k) {
+                if (v1[k]) {
+                    if (t1[k] == u) r1[k] = hu;  // the held row (pair 1's input, pre-update)
+                    else r1[k].load(a.node + (int64_t)t1[k] * d, lane, d);
+                }
+                if (v2[k] && t2[k] != v) r2[k].load(a.node + (int64_t)t2[k] * d, lane, d);
+            }
+            r1[0] = v != u ? in2 : hu;  // pair 1's positive node[v] (pre-update)
+            // pair 1: input = the held u
+            {
+                float part[MAXN + 1];
+#pragma unroll
+                for (int k = 0; k <= MAXN; ++k) part[k] = v1[k] ? lane_partial(hu, r1[k]) : 0.0f;
+                wave_sum_n(part, n + 1);
+                R work;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) work.v[q] = 0.0f;
+#pragma unroll
+                for (int k = 0; k <= MAXN; ++k) {
+                    if (!v1[k]) continue;
+                    float sig;
+                    if (!sigmoid_ref(uniformf(part[k]), &sig)) continue;
+                    const float g = ((k == 0 ? 1.0f : 0.0f) - sig) * a.lr;  // pyx:243
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) work.v[q] = __builtin_fmaf(g, r1[k].v[q], work.v[q]);
+                }
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    hu.v[q] = hu.v[q] + work.v[q];  // pyx:247
+                    du.v[q] = du.v[q] + work.v[q];
+                }
+            }
+            // pair 2: input v, positive = the held u as pair 1 left it; a self-loop's input is
+            // that row too; a negative equal to v reads v before pair 2's update
+            r2[0] = hu;
+            if (v == u) in2 = hu;
+#pragma unroll
+            for (int k = 1; k <= MAXN; ++k)
+                if (v2[k] && t2[k] == v) r2[k] = in2;
+            {
+                float part[MAXN + 1];
+#pragma unroll
+                for (int k = 0; k <= MAXN; ++k) part[k] = v2[k] ? lane_partial(in2, r2[k]) : 0.0f;
+                wave_sum_n(part, n + 1);
+                R work;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) work.v[q] = 0.0f;
+#pragma unroll
+                for (int k = 0; k <= MAXN; ++k) {
+                    if (!v2[k]) continue;
+                    float sig;
+                    if (!sigmoid_ref(uniformf(part[k]), &sig)) continue;
+                    const float g = ((k == 0 ? 1.0f : 0.0f) - sig) * a.lr;
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) work.v[q] = __builtin_fmaf(g, r2[k].v[q], work.v[q]);
+                }
+                if (v == u) {  // self-loop: pair 2 updates the held row itself
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) {
+                        hu.v[q] = hu.v[q] + work.v[q];
+                        du.v[q] = du.v[q] + work.v[q];
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) in2.v[q] = in2.v[q] + work.v[q];
+                    if (hot_v) work.atomic_add(a.node + (int64_t)v * d, lane, d);
+                    else in2.store(a.node + (int64_t)v * d, lane, d);
+                }
+            }
+        }
+        flush();
+    }
+}
+
 struct KernelSet {
     void *o2_direct[2][3];  // [FULL][maxn idx]
     void *o2_ring[2][3];    // sequential mode
     void *o2_stream[2][3];  // Hogwild mode
     void *o1[2][3];
+    void *o1_runs[2][3];
 };
 #define COME_DECLARE_VEC(V) \
     const KernelSet &kernels_vec##V(); \

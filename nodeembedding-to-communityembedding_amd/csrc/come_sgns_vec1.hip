@@ -8,14 +8,17 @@ const KernelSet &kernels_vec1() {
         KernelSet k{};
         k.o2_direct[0][0] = (void *)&k_sgns_o2<1, false, 5>;
         k.o1[0][0] = (void *)&k_sgns_o1<1, false, 5>;
+        k.o1_runs[0][0] = (void *)&k_sgns_o1_runs<1, false, 5>;
         k.o2_ring[0][0] = (void *)&k_sgns_o2_ring<1, false, 5>;
         k.o2_stream[0][0] = (void *)&k_sgns_o2_stream<1, false, 5>;
         k.o2_direct[0][1] = (void *)&k_sgns_o2<1, false, 10>;
         k.o1[0][1] = (void *)&k_sgns_o1<1, false, 10>;
+        k.o1_runs[0][1] = (void *)&k_sgns_o1_runs<1, false, 10>;
         k.o2_ring[0][1] = (void *)&k_sgns_o2_ring<1, false, 10>;
         k.o2_stream[0][1] = (void *)&k_sgns_o2_stream<1, false, 10>;
         k.o2_direct[0][2] = (void *)&k_sgns_o2<1, false, 20>;
         k.o1[0][2] = (void *)&k_sgns_o1<1, false, 20>;
+        k.o1_runs[0][2] = (void *)&k_sgns_o1_runs<1, false, 20>;
         k.o2_ring[0][2] = (void *)&k_sgns_o2_ring<1, false, 20>;
         k.o2_stream[0][2] = (void *)&k_sgns_o2_stream<1, false, 20>;
         return k;

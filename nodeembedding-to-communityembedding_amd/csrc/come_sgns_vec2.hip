@@ -8,26 +8,32 @@ const KernelSet &kernels_vec2() {
         KernelSet k{};
         k.o2_direct[0][0] = (void *)&k_sgns_o2<2, false, 5>;
         k.o1[0][0] = (void *)&k_sgns_o1<2, false, 5>;
+        k.o1_runs[0][0] = (void *)&k_sgns_o1_runs<2, false, 5>;
         k.o2_ring[0][0] = (void *)&k_sgns_o2_ring<2, false, 5>;
         k.o2_stream[0][0] = (void *)&k_sgns_o2_stream<2, false, 5>;
         k.o2_direct[0][1] = (void *)&k_sgns_o2<2, false, 10>;
         k.o1[0][1] = (void *)&k_sgns_o1<2, false, 10>;
+        k.o1_runs[0][1] = (void *)&k_sgns_o1_runs<2, false, 10>;
         k.o2_ring[0][1] = (void *)&k_sgns_o2_ring<2, false, 10>;
         k.o2_stream[0][1] = (void *)&k_sgns_o2_stream<2, false, 10>;
         k.o2_direct[0][2] = (void *)&k_sgns_o2<2, false, 20>;
         k.o1[0][2] = (void *)&k_sgns_o1<2, false, 20>;
+        k.o1_runs[0][2] = (void *)&k_sgns_o1_runs<2, false, 20>;
         k.o2_ring[0][2] = (void *)&k_sgns_o2_ring<2, false, 20>;
         k.o2_stream[0][2] = (void *)&k_sgns_o2_stream<2, false, 20>;
         k.o2_direct[1][0] = (void *)&k_sgns_o2<2, true, 5>;
         k.o1[1][0] = (void *)&k_sgns_o1<2, true, 5>;
+        k.o1_runs[1][0] = (void *)&k_sgns_o1_runs<2, true, 5>;
         k.o2_ring[1][0] = (void *)&k_sgns_o2_ring<2, true, 5>;
         k.o2_stream[1][0] = (void *)&k_sgns_o2_stream<2, true, 5>;
         k.o2_direct[1][1] = (void *)&k_sgns_o2<2, true, 10>;
         k.o1[1][1] = (void *)&k_sgns_o1<2, true, 10>;
+        k.o1_runs[1][1] = (void *)&k_sgns_o1_runs<2, true, 10>;
         k.o2_ring[1][1] = (void *)&k_sgns_o2_ring<2, true, 10>;
         k.o2_stream[1][1] = (void *)&k_sgns_o2_stream<2, true, 10>;
         k.o2_direct[1][2] = (void *)&k_sgns_o2<2, true, 20>;
         k.o1[1][2] = (void *)&k_sgns_o1<2, true, 20>;
+        k.o1_runs[1][2] = (void *)&k_sgns_o1_runs<2, true, 20>;
         k.o2_ring[1][2] = (void *)&k_sgns_o2_ring<2, true, 20>;
         k.o2_stream[1][2] = (void *)&k_sgns_o2_stream<2, true, 20>;
         return k;

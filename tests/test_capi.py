@@ -66,6 +66,7 @@ def test_launch_options_snapshot_and_per_call_struct():
     o = _lib.launch_opts()
     assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 3
     assert o.gmm_resp16 == 2
+    assert o.o1_chunk == -1
     assert o.o2_update_count is None
     _lib.set_option("max_waves", 77)
     try:
@@ -78,7 +79,7 @@ def test_launch_options_snapshot_and_per_call_struct():
         _lib.set_option("no_such_knob", 1)
     with pytest.raises(ValueError):
         _lib.launch_opts(no_such_knob=1)
-    assert ctypes.sizeof(_lib.LaunchOpts) == 15 * 4 + 4 + 8  # 15 ints, padding, the pointer
+    assert ctypes.sizeof(_lib.LaunchOpts) == 17 * 4 + 4 + 8  # 17 ints, padding, the pointer
     p = ctypes.c_void_p(0)
     rc = L.come_sgns_o2_ex(p, p, 0, 128, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p,
                            ctypes.byref(o), p)

@@ -313,14 +313,27 @@ def test_o1_kat_bit_exact_vs_oracle_and_golden(name):
 
 @pytest.mark.parametrize("d,neg,V,E", [(128, 5, 5000, 3000), (2, 4, 34, 78), (256, 10, 300, 500),
                                        (100, 20, 50, 200), (128, 5, 3, 50), (512, 1, 100, 64)])
-def test_o1_random_bit_exact_vs_oracle(d, neg, V, E):
+@pytest.mark.parametrize("chunk", [0, 7, -1])
+def test_o1_random_bit_exact_vs_oracle(d, neg, V, E, chunk):
+    """Sequential mode vs the oracle bit for bit: the per-edge kernel (chunk 0) and the run kernel
+    k_sgns_o1_runs (o1_chunk = 7: the input row held over runs of edges sharing it; edges sorted
+    by their first endpoint so runs form, self-loops and negatives equal to the held row
+    included; o1_chunk = -1, the default: one chunk of every edge in order)."""
+    from come_amd import _lib
     rng = np.random.RandomState(d + neg + V)
     table = orc.make_table(rng.randint(1, 30, V), 5 * V + 7)
     node0 = rng.uniform(-0.5, 0.5, (V, d)).astype(np.float32)
     edges = rng.randint(0, V, (E, 2)).astype(np.int32)
     edges[::17, 1] = edges[::17, 0]  # self loops
+    if chunk:
+        edges = edges[np.argsort(edges[:, 0], kind="stable")]
     seeds = rng.randint(0, 2 ** 48, E, dtype=np.int64).astype(np.uint64)
-    node = run_o1(node0, edges, seeds, neg, table, 0.2)
+    prev = _lib.launch_opts().o1_chunk
+    _lib.set_option("o1_chunk", chunk)
+    try:
+        node = run_o1(node0, edges, seeds, neg, table, 0.2)
+    finally:
+        _lib.set_option("o1_chunk", prev)
     n_ref = node0.copy()
     orc.sgns_o1(n_ref, edges, seeds, neg, table, 0.2, dot_mode=orc.DOT_WAVE64)
     np.testing.assert_array_equal(node, n_ref)

@@ -240,6 +240,45 @@ def test_o1_hogwild_heldout_loss_matches_sequential_oracle(c2_shape):
         assert abs(a - b) / abs(b) < 0.01, (l_hog, l_seq)  # SURVEY.md §8c tier C
 
 
+def test_o1_hogwild_in_reference_edge_order(c2_shape):
+    """O1 tier C in the reference's own edge order (np.array(G.edges()), node_embeddings.py:39:
+    grouped by the first endpoint, so consecutive edges share their input row) at the product
+    default o1_chunk = -1 (k_sgns_o1_runs, one contiguous chunk per wavefront: the edges in flight
+    spread over the whole list), against the sequential oracle on the same order: held-out losses
+    within 1%.  Measured r04q: -1 +0.23%; the per-edge kernel (o1_chunk 0, the
+    wavefronts in flight on ~24k consecutive edges sharing a few hundred input rows) +1.59%, and
+    o1_chunk 16 +1.52% -- both outside tier C in this order, which is why -1 is the default."""
+    from come_amd import _lib
+    g, table, train, held, node0, seeds = c2_shape
+    train = train[np.lexsort((train[:, 1], train[:, 0]))]  # G.edges() order of the kept edges
+    n, lr = 5, 0.1
+    rng = np.random.RandomState(32)
+    neg = table[rng.randint(0, len(table), (len(held), n))].astype(np.int64)
+
+    def losses(x):
+        ref = float(-log_sigmoid(np.einsum("pd,pd->p", x[held[:, 1]].astype(np.float64),
+                                           x[held[:, 0]].astype(np.float64))).sum())
+        return ref, sgns_loss(x, x, held[:, 0], held[:, 1], neg)
+
+    node = dev(node0)
+    tab = dev(table)
+    hot = tsi.hot_rows(tab, g.V, int(tsi.DEFAULT_HOT_P * len(table)))
+    chunk = _lib.launch_opts().o1_chunk
+    assert chunk == -1
+    tsi.sgns_o1(node, dev(train), dev(seeds), n, tab, lr, tsi.MODE_HOGWILD, hot=hot)
+    torch.cuda.synchronize()
+    hog = node.cpu().numpy()
+    assert np.isfinite(hog).all()
+    l_hog = losses(hog)
+    seq = node0.copy()
+    orc.sgns_o1_hogwild(seq, train, seeds, n, table, lr, threads=1)
+    l_seq = losses(seq)
+    print("O1 G.edges() order, chunk %d: held-out loss (reference :26-31 / SGNS) seq %.1f / %.5f "
+          "gpu-hogwild %.1f / %.5f" % ((chunk,) + l_seq + l_hog))
+    for a, b in zip(l_hog, l_seq):
+        assert abs(a - b) / abs(b) < 0.01, (l_hog, l_seq)  # SURVEY.md §8c tier C
+
+
 def test_hot_rows_bitmap_matches_table_counts():
     """come_hot_rows: bit r set iff row r holds >= min_count slots (numpy bincount), on a
     make_table table (long uniform runs) and on an unsorted table (per-lane counting)."""
