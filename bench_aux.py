@@ -180,7 +180,8 @@ def c4(args):
         if ct16 else 1.0
     cov_kernel = ({3: "k_gmm_cov16", 0: "k_gmm_cov_mfma"}.get(opts.gmm_cov_async, "k_gmm_cov_async")
                   if ct16 else "VALU")
-    resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp16" if opts.gmm_resp16
+    resp_kernel = ("k_gmm_resp16p" if opts.gmm_resp16 == 3 else
+                   "k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp16" if opts.gmm_resp16
                    else "k_gmm_resp_db" if opts.gmm_resp_db else "k_gmm_resp_mfma") if ct16 \
         else "VALU"
     x0 = x.clone()

@@ -265,10 +265,13 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *   gmm_resp16          GMM E-step at d = 64, 128 on 16x16x4 MFMAs (16-wide triangular skip,
  *                       in-lane row sums): default 2 = k_gmm_resp16t (the factors' non-zero
  *                       16x16 blocks packed, whole components double-buffered, one barrier per
- *                       component; a launch holding a lower or dense factor runs every block);
- *                       1 = k_gmm_resp16 (balanced half images, two barriers per component);
- *                       0 = the 32x32x2 kernels of gmm_resp_db.  2 / 1 / 0: 7.13 / 7.24 / 8.25 ms
- *                       at C4
+ *                       component; one 16-row tile per wavefront, 8 per workgroup; a launch
+ *                       holding a lower or dense factor runs every block, in k_gmm_resp16_full);
+ *                       16 + i = k_gmm_resp16t variant i (A/B: 16 two row tiles per wavefront,
+ *                       bit-identical to 2; 17 = 16 with a packed-fp32 epilogue; 18 = 2;
+ *                       19 = 2 with the packed epilogue); 1 = k_gmm_resp16 (balanced half
+ *                       images, two barriers per component); 0 = the 32x32x2 kernels of
+ *                       gmm_resp_db.  2 / 16 / 1 / 0: 7.00 / 7.10 / 7.24 / 8.25 ms at C4
  *   o1_chunk            O1: > 0 = one wavefront per chunk of that many consecutive edges, the
  *                       input row held in registers over each run of edges sharing it
  *                       (k_sgns_o1_runs); default -1 = one contiguous chunk per wavefront of the

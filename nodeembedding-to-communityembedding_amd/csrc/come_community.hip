@@ -1010,14 +1010,14 @@ __device__ __forceinline__ void r16_phase(
 // FULL: every component runs every (quad, tile) block -- the launch holds some lower or dense
 // factor (flags[K], k_gmm_lower_flags); else the upper-triangular skip for all components.
 template <int D, bool FULL>
-__device__ __forceinline__ void r16_body(const RespArgs &a, float *sm) {
+__device__ __forceinline__ void r16_body(const RespArgs &a, float *sm, int64_t blk) {
     using RS = Resp16Shape<D>;
     constexpr int NQ = RS::NQ;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int j16 = lane & 15, kg = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * 128 + wid * 32;
+    const int64_t row0 = blk * 128 + wid * 32;
     f32x4 xb[2][NQ];  // xb[rt][q][t] = x[row0 + 16 rt + j16][16 q + 4 kg + t]
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
@@ -1103,9 +1103,9 @@ template <int D>
 __global__ void __launch_bounds__(256, 2) k_gmm_resp16(RespArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0)
-        r16_body<D, true>(a, sm);
+        r16_body<D, true>(a, sm, blockIdx.x);
     else
-        r16_body<D, false>(a, sm);
+        r16_body<D, false>(a, sm, blockIdx.x);
 }
 
 // ---- k_gmm_resp16 on packed upper factors: one barrier per component ---------------------------
@@ -1149,14 +1149,28 @@ __global__ void __launch_bounds__(256) k_pack_upper16(const float *__restrict__ 
     }
 }
 
-template <int D>
+// Shape of a k_gmm_resp16t variant: VT & 8 = one 16-row tile per wavefront and 8 wavefronts per
+// 128-row workgroup (91-95 VGPRs: 4 waves per SIMD instead of 2 -- the LDS holds two workgroups
+// per CU either way -- at twice the A-operand reads per MFMA); else two row tiles per wavefront
+// and 4 wavefronts (216 VGPRs).
+template <int VT>
+struct R16tShape {
+    static constexpr int RT = (VT & 8) ? 1 : 2;  // 16-row tiles per wavefront
+    static constexpr int NW = 8 / RT;            // wavefronts per workgroup
+    static constexpr int ROWS = 16 * RT * NW;    // rows per workgroup (128)
+    static constexpr int THREADS = 64 * NW;
+    static constexpr int WPE = 2 * (3 - RT);     // waves per SIMD the registers must allow: 4 / 2
+};
+
+// C: the calling kernel (one instantiation each: see r16_stage_mp); NW wavefronts share the copy
+template <int D, int C, int NW>
 __device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf, int wid,
                                            int lane) {
     using T = Resp16T<D>;
     const float *src = a.prec_t + (int64_t)k * T::TRI;  // the packed blocks in this body
 #pragma unroll
-    for (int j = 0; j < (T::PIECES + 3) / 4; ++j) {
-        const int i = wid + 4 * j;
+    for (int j = 0; j < (T::PIECES + NW - 1) / NW; ++j) {
+        const int i = wid + NW * j;
         if (i >= T::PIECES) break;  // wavefront-uniform
         __builtin_amdgcn_global_load_lds(src + i * 256 + lane * 4, buf + i * 256, 16, 0, 0);
     }
@@ -1186,50 +1200,155 @@ struct TriBlocks {
     }
 };
 
-// All 36 (d = 128) upper blocks of one component on both row tiles, in row-major order (q, ct >=
-// q); A operands read two blocks ahead through a 3-slot ring.
-template <int D>
+// All 36 (d = 128) upper blocks of one component on the wavefront's RT row tiles, in row-major
+// order (q, ct >= q); A operands read two blocks ahead through a 3-slot ring.  `after_first` runs
+// once the first A operands are requested (VT & 4: the next component's staging issued behind
+// them).  VT & 1: blocks taken in pairs, the accumulation chains of a pair interleaved.
+template <int D, int VT, typename F>
 __device__ __forceinline__ void r16t_blocks(
-    const __attribute__((ext_vector_type(4))) float (&xb)[2][D / 16], const float *buf, int abase,
-    __attribute__((ext_vector_type(4))) float (&acc)[2][D / 16]) {
+    const __attribute__((ext_vector_type(4))) float (&xb)[R16tShape<VT>::RT][D / 16],
+    const float *buf, int abase,
+    __attribute__((ext_vector_type(4))) float (&acc)[R16tShape<VT>::RT][D / 16],
+    F &&after_first) {
     using T = Resp16T<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int NQ = T::NQ;
+    constexpr int NQ = T::NQ, RT = R16tShape<VT>::RT;
     constexpr int NB = NQ * (NQ + 1) / 2;
     constexpr TriBlocks<NQ> TB{};
     auto fetch = [&](int n) {
         return *reinterpret_cast<const f32x4 *>(buf + T::off(TB.q[n]) + (TB.ct[n] - TB.q[n]) * 256 +
                                                 abase);
     };
-    f32x4 av[3];
-    av[0] = fetch(0);
-    av[1] = fetch(1);
+    if constexpr ((VT & 1) == 0) {
+        f32x4 av[3];
+        av[0] = fetch(0);
+        av[1] = fetch(1);
+        after_first();
 #pragma unroll
-    for (int n = 0; n < NB; ++n) {
-        if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
-        const int q = TB.q[n], ct = TB.ct[n];
+        for (int n = 0; n < NB; ++n) {
+            if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
+            const int q = TB.q[n], ct = TB.ct[n];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[rt][q][t],
-                                                                   acc[rt][ct], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+                for (int rt = 0; rt < RT; ++rt)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[rt][q][t],
+                                                                       acc[rt][ct], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        static_assert(NB % 2 == 0, "pairs of blocks");
+        f32x4 av[4];  // two pairs: the current one and the next
+        av[0] = fetch(0);
+        av[1] = fetch(1);
+        after_first();
+#pragma unroll
+        for (int n = 0; n < NB; n += 2) {
+            if (n + 2 < NB) {
+                av[(n + 2) % 4] = fetch(n + 2);
+                av[(n + 3) % 4] = fetch(n + 3);
+            }
+            const int q0 = TB.q[n], c0 = TB.ct[n], q1 = TB.q[n + 1], c1 = TB.ct[n + 1];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+                    acc[rt][c0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 4][t], xb[rt][q0][t],
+                                                                       acc[rt][c0], 0, 0, 0);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+                    acc[rt][c1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        av[(n + 1) % 4][t], xb[rt][q1][t], acc[rt][c1], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
 }
 
-template <int D>
+// log N(x_row; mu_k, P_k) of the lane's row (row tile kg & 1 when RT = 2) for the component in
+// `buf`.  VT & 2: the epilogue on packed fp32 (v_pk_fma: even and odd columns summed apart, then
+// added -- its own rounding).
+template <int D, int VT, typename F>
+__device__ __forceinline__ float r16t_lp(
+    const __attribute__((ext_vector_type(4))) float (&xb)[R16tShape<VT>::RT][D / 16],
+    const float *buf, int abase, int kg, F &&after_first) {
+    using T = Resp16T<D>;
+    constexpr int NQ = T::NQ, RT = R16tShape<VT>::RT;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    using f32x2 = __attribute__((ext_vector_type(2))) float;
+    const float lnk = buf[T::PAR + 1];
+    f32x4 acc[RT][NQ];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    r16t_blocks<D, VT>(xb, buf, abase, acc, after_first);
+    float sq[RT];
+    if constexpr ((VT & 2) == 0) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) sq[rt] = 0.0f;
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) {
+            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float y = acc[rt][ct][e] - mp[e];
+                    sq[rt] = __builtin_fmaf(y, y, sq[rt]);
+                }
+        }
+    } else {
+        f32x2 s2[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) s2[rt] = f32x2{0.0f, 0.0f};
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) {
+            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x2 y = f32x2{acc[rt][ct][2 * h], acc[rt][ct][2 * h + 1]} -
+                                    f32x2{mp[2 * h], mp[2 * h + 1]};
+                    s2[rt] = __builtin_elementwise_fma(y, y, s2[rt]);
+                }
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) sq[rt] = s2[rt][0] + s2[rt][1];
+    }
+    const float tot0 = reduce_stage<5>(reduce_stage<4>(sq[0]));
+    if constexpr (RT == 1) {
+        return lnk - 0.5f * tot0;
+    } else {
+        const float tot1 = reduce_stage<5>(reduce_stage<4>(sq[1]));
+        return lnk - 0.5f * ((kg & 1) ? tot1 : tot0);
+    }
+}
+
+// online log-sum-exp step
+__device__ __forceinline__ void lse_push(float lp, float &run_max, float &run_sum) {
+    if (lp > run_max) {
+        run_sum = run_sum * expf(run_max - lp) + 1.0f;
+        run_max = lp;
+    } else {
+        run_sum += expf(lp - run_max);
+    }
+}
+
+template <int D, int VT>
 __device__ __forceinline__ void r16t_body(const RespArgs &a, float *sm) {
     using T = Resp16T<D>;
-    constexpr int NQ = T::NQ;
+    using S = R16tShape<VT>;
+    constexpr int NQ = T::NQ, RT = S::RT;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int j16 = lane & 15, kg = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * 128 + wid * 32;
-    f32x4 xb[2][NQ];
+    const int64_t row0 = (int64_t)blockIdx.x * S::ROWS + wid * 16 * RT;
+    f32x4 xb[RT][NQ];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
         const int64_t row = row0 + 16 * rt + j16;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -1237,46 +1356,27 @@ __device__ __forceinline__ void r16t_body(const RespArgs &a, float *sm) {
             if (row < a.V) xb[rt][q] = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg);
         }
     }
-    r16t_stage<D>(a, 0, sm, wid, lane);
+    r16t_stage<D, VT, S::NW>(a, 0, sm, wid, lane);
     // the lane's A operands of block (q, ct): row ct*16 + j16 of quad q's row block
     const int abase = j16 * 16 + 4 * (kg ^ ((j16 >> 1) & 2));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int64_t my_row = row0 + 16 * (kg & 1) + j16;
-    const bool owner = kg < 2 && my_row < a.V;
+    // RT = 2: lanes 0-15 own row tile 0, lanes 16-31 row tile 1; RT = 1: lanes 0-15
+    const int64_t my_row = row0 + (RT == 2 ? 16 * (kg & 1) : 0) + j16;
+    const bool owner = kg < RT && my_row < a.V;
     float run_max = -INFINITY, run_sum = 0.0f;
     for (int k = 0; k < a.K; ++k) {
         const float *buf = sm + (k & 1) * T::BUF;
-        if (k + 1 < a.K) r16t_stage<D>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
-        const float lnk = buf[T::PAR + 1];
-        f32x4 acc[2][NQ];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        r16t_blocks<D>(xb, buf, abase, acc);
-        float sq[2] = {0.0f, 0.0f};
-#pragma unroll
-        for (int ct = 0; ct < NQ; ++ct) {
-            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float y = acc[rt][ct][e] - mp[e];
-                    sq[rt] = __builtin_fmaf(y, y, sq[rt]);
-                }
-        }
-        const float tot0 = reduce_stage<5>(reduce_stage<4>(sq[0]));
-        const float tot1 = reduce_stage<5>(reduce_stage<4>(sq[1]));
-        const float lp = lnk - 0.5f * ((kg & 1) ? tot1 : tot0);
+        auto stage_next = [&] {
+            if (k + 1 < a.K)
+                r16t_stage<D, VT, S::NW>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
+        };
+        if constexpr ((VT & 4) == 0) stage_next();
+        const float lp = r16t_lp<D, VT>(xb, buf, abase, kg, [&] {
+            if constexpr ((VT & 4) != 0) stage_next();
+        });
         if (owner) a.resp[my_row * a.K + k] = lp;
-        if (lp > run_max) {
-            run_sum = run_sum * expf(run_max - lp) + 1.0f;
-            run_max = lp;
-        } else {
-            run_sum += expf(lp - run_max);
-        }
+        lse_push(lp, run_max, run_sum);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
     }
@@ -1289,17 +1389,32 @@ __device__ __forceinline__ void r16t_body(const RespArgs &a, float *sm) {
 }
 
 // gmm_resp16 = 2: the packed, one-barrier form when every factor is upper-triangular (flags[K] ==
-// 0), else k_gmm_resp16's FULL body; prec_t points to the packed blocks, prec_full to P^T.
-template <int D>
-__global__ void __launch_bounds__(256, 2) k_gmm_resp16t(RespArgs a) {
+// 0), else k_gmm_resp16's FULL body (on the first four wavefronts; with 8, the others run it
+// with no rows so that every barrier is met); prec_t points to the packed blocks, prec_full to P^T.
+template <int D, int VT>
+__global__ void __launch_bounds__(R16tShape<VT>::THREADS, R16tShape<VT>::WPE)
+    k_gmm_resp16t(RespArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0) {
-        RespArgs b = a;
-        b.prec_t = a.prec_full;
-        r16_body<D, true>(b, sm);
+        if constexpr (R16tShape<VT>::RT == 2) {
+            RespArgs b = a;
+            b.prec_t = a.prec_full;
+            r16_body<D, true>(b, sm, blockIdx.x);
+        }
     } else {
-        r16t_body<D>(a, sm);
+        r16t_body<D, VT>(a, sm);
     }
+}
+
+// The FULL body for the one-row-tile variants (whose registers cannot hold it), launched after
+// them: a no-op unless the launch holds a lower or dense factor (flags[K]); row blocks grid-stride.
+template <int D>
+__global__ void __launch_bounds__(256, 2) k_gmm_resp16_full(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) == 0) return;
+    RespArgs b = a;
+    b.prec_t = a.prec_full;
+    for (int64_t blk = blockIdx.x; blk * 128 < a.V; blk += gridDim.x) r16_body<D, true>(b, sm, blk);
 }
 
 // ---- GMM M-step scatter matrices -------------------------------------------------------------
@@ -2228,7 +2343,18 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         rc = hip_error(hipGetLastError(), "k_transpose_sq launch");
         if (rc) return rc;
         a.prec_t = pt;
-        if (current_opts().gmm_resp16 == 2) {
+        const int r16 = current_opts().gmm_resp16;
+        // k_gmm_resp16t variants (VT): 0 = two row tiles per wavefront, 2 = + packed epilogue,
+        // 8 = one row tile (the default: 7.00 vs 7.10 ms at C4, bit-identical to 0), 10 = one row
+        // tile + packed epilogue (7.01 ms; profiles/r04_ab_estep16.txt; 10-wavefront workgroups
+        // of VT 8: 8.7 ms).  gmm_resp16 = 2: VT 8; 16 + i: entry i (A/B)
+        static const int kVts[4] = {0, 2, 8, 10};
+        static void (*const k_r16t[4][2])(RespArgs) = {
+            {k_gmm_resp16t<64, 0>, k_gmm_resp16t<128, 0>},
+            {k_gmm_resp16t<64, 2>, k_gmm_resp16t<128, 2>},
+            {k_gmm_resp16t<64, 8>, k_gmm_resp16t<128, 8>},
+            {k_gmm_resp16t<64, 10>, k_gmm_resp16t<128, 10>}};
+        if (r16 == 2 || (r16 >= 16 && r16 < 20)) {
             const int tri = d == 64 ? Resp16T<64>::TRI : Resp16T<128>::TRI;
             float *packed = stream_scratch(dev, stream, kScratchGmmTri, sizeof(float) * (size_t)K * tri);
             if (!packed) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
@@ -2245,16 +2371,29 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
                 d == 64 ? Resp16Shape<64>::LDS : Resp16Shape<128>::LDS);
             static bool attr16t = false;
             if (!attr16t) {
-                (void)hipFuncSetAttribute((const void *)k_gmm_resp16t<64>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                (void)hipFuncSetAttribute((const void *)k_gmm_resp16t<128>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                for (int v = 0; v < 4; ++v)
+                    for (int dd = 0; dd < 2; ++dd)
+                        (void)hipFuncSetAttribute((const void *)k_r16t[v][dd],
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  160 * 1024);
+                for (void (*f)(RespArgs) : {k_gmm_resp16_full<64>, k_gmm_resp16_full<128>})
+                    (void)hipFuncSetAttribute((const void *)f,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr16t = true;
             }
-            hipLaunchKernelGGL(d == 64 ? k_gmm_resp16t<64> : k_gmm_resp16t<128>,
-                               dim3((unsigned)((V + 127) / 128)), dim3(256), ldst,
-                               (hipStream_t)stream, b);
-            return hip_error(hipGetLastError(), "k_gmm_resp16t launch");
+            const int vi = r16 >= 16 ? r16 - 16 : 2;
+            const int vt = kVts[vi];
+            hipLaunchKernelGGL(k_r16t[vi][d == 64 ? 0 : 1], dim3((unsigned)((V + 127) / 128)),
+                               dim3((vt & 8) ? 512 : 256), ldst, (hipStream_t)stream, b);
+            rc = hip_error(hipGetLastError(), "k_gmm_resp16t launch");
+            if (rc || !(vt & 8)) return rc;
+            const int64_t blks = (V + 127) / 128;
+            const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
+                                                                   : Resp16Shape<128>::LDS);
+            hipLaunchKernelGGL(d == 64 ? k_gmm_resp16_full<64> : k_gmm_resp16_full<128>,
+                               dim3((unsigned)std::min<int64_t>(blks, 2 * (int64_t)num_cus(dev))),
+                               dim3(256), lds16, (hipStream_t)stream, b);
+            return hip_error(hipGetLastError(), "k_gmm_resp16_full launch");
         }
         if (current_opts().gmm_resp16) {
             const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS

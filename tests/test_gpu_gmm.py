@@ -81,14 +81,17 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("variant", [0, 3, "16", "16t"])
+@pytest.mark.parametrize("variant", [0, 3, "16", "16t", "16t0"])
 def test_estep_mixed_factor_shapes(d, variant):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
     loop.  Mixed in one launch, every component must match the float64 quadratic form -- for
     k_gmm_resp_mfma (variant 0), the staggered double-buffered kernel whose accumulators start
     at -mu_k P_k (gmm_resp_db = 3) and the 16x16x4 kernel k_gmm_resp16 (gmm_resp16 = 1; a lower
-    or dense factor in the launch makes it run every block of every component)."""
+    or dense factor in the launch makes it run every block of every component), and its packed
+    form k_gmm_resp16t: the default one-row-tile variant (gmm_resp16 = 2), whose FULL case is
+    the separate k_gmm_resp16_full launch, and the two-row-tile one (= 16), which holds the
+    FULL body itself."""
     from come_amd import _lib
     V, K = 1500, 6
     rng = np.random.RandomState(d)
@@ -104,7 +107,7 @@ def test_estep_mixed_factor_shapes(d, variant):
     ln = np.log(np.full(K, 1.0 / K))
     mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    r16 = {"16": 1, "16t": 2}.get(variant, 0)
+    r16 = {"16": 1, "16t": 2, "16t0": 16}.get(variant, 0)
     with opts(gmm_resp16=r16, gmm_resp_db=0 if r16 else variant):
         resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
@@ -113,6 +116,32 @@ def test_estep_mixed_factor_shapes(d, variant):
     ref_lse = logsumexp(lp, 1)
     np.testing.assert_allclose(resp.cpu().numpy(), np.exp(lp - ref_lse[:, None]), atol=2e-4)
     np.testing.assert_allclose(lse.cpu().numpy(), ref_lse, rtol=2e-5, atol=2e-3)
+
+
+@pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (70_001, 7, 64), (300, 3, 64), (129, 1, 128),
+                                   (1, 4, 128), (5000, 2, 128)])
+def test_estep16t_variants_bit_identical(V, K, d):
+    """k_gmm_resp16t's wave shapes change no arithmetic: two row tiles per wavefront (gmm_resp16 =
+    16, VT 0) equals one (the default 2 = VT 8) bit for bit, and so do the packed-fp32-epilogue
+    forms (17, VT 2 and 19, VT 10), ragged row counts included."""
+    rng = np.random.RandomState(V + 7 * K)
+    X = rng.standard_normal((V, d)).astype(np.float32)
+    P = np.stack([np.triu(rng.standard_normal((d, d)) / np.sqrt(d)) + 2 * np.eye(d)
+                  for _ in range(K)])
+    mu = rng.standard_normal((K, d)) * 0.3
+    mp = np.einsum("kd,kde->ke", mu, P)
+    ln = np.log(rng.dirichlet(np.ones(K)))
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
+    out = {}
+    for r16 in (16, 2, 17, 19):
+        with opts(gmm_resp16=r16):
+            resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
+        out[r16] = resp.cpu().numpy(), lse.cpu().numpy()
+    for a, b in ((2, 16), (19, 17)):
+        np.testing.assert_array_equal(out[a][0], out[b][0])
+        np.testing.assert_array_equal(out[a][1], out[b][1])
+    assert np.isfinite(out[2][0]).all() and np.abs(out[2][0].sum(1) - 1).max() < 1e-4
+    np.testing.assert_allclose(out[19][0], out[2][0], atol=1e-4)  # own rounding: even/odd sums
 
 
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
@@ -296,7 +325,7 @@ def test_estep_double_buffered_kernel_bit_identical(V, K, d):
 
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (1000, 5, 128), (2049, 9, 64), (300, 3, 64),
                                    (129, 1, 128)])
-@pytest.mark.parametrize("r16", [1, 2])
+@pytest.mark.parametrize("r16", [1, 2, 16, 17, 19])
 def test_estep16_upper_factors_vs_float64(V, K, d, r16):
     """k_gmm_resp16 (gmm_resp16 = 1) and its packed one-barrier form k_gmm_resp16t (= 2) with
     sklearn-shaped (upper-triangular) precision factors only -- the launches that take the 16-wide
