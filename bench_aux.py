@@ -180,8 +180,11 @@ def c4(args):
         if ct16 else 1.0
     cov_kernel = ({3: "k_gmm_cov16", 0: "k_gmm_cov_mfma"}.get(opts.gmm_cov_async, "k_gmm_cov_async")
                   if ct16 else "VALU")
-    resp_kernel = ("k_gmm_resp16p" if opts.gmm_resp16 == 3 else
-                   "k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp16" if opts.gmm_resp16
+    comm_kernel = ({2: "k_community16", 0: "k_community_mfma"}.get(opts.community_async,
+                                                                   "k_community_async")
+                   if ct16 else "VALU")
+    resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 or 16 <= opts.gmm_resp16 < 20
+                   else "k_gmm_resp16" if opts.gmm_resp16
                    else "k_gmm_resp_db" if opts.gmm_resp_db else "k_gmm_resp_mfma") if ct16 \
         else "VALU"
     x0 = x.clone()
@@ -266,6 +269,7 @@ def c4(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": tg * 1e3,
         "higher_is_better": True, "dtype": "f32", "data": "synthetic N(0,1) rows, random SPD",
         "config": {"workload": "configs[3]/C4: V=%d K=%d d=%d" % (V, K, d),
+                   "community_kernel": comm_kernel,
                    # E-step / scatter: 2 V K d^2 algorithmic flops, of which the kernels execute
                    # only the upper-triangular / symmetric blocks (fractions above)
                    "gmm_resp_kernel": resp_kernel, "gmm_resp_blocks_executed": tri_resp,

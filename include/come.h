@@ -248,7 +248,9 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *   max_waves           absolute cap on wavefronts in flight (0 = none)
  *   o1_blocks_per_cu    O1 grid cap in 4-wave workgroups per CU (0 = 6)
  *   resident_cap        1 = also clamp grids to the workgroups the occupancy API reports resident
- *   community_async     default 1: k_community_async; 0 = synchronous-staging k_community_mfma
+ *   community_async     default 2: k_community16 (16x16x4 MFMAs, one 16-row tile per
+ *                       wavefront, 4 waves per SIMD; 11.57 vs 12.46 ms at C4); 1: k_community_async
+ *                       (32x32x2, 2 waves per SIMD); 0 = synchronous-staging k_community_mfma
  *   gmm_cov_async       default 3: k_gmm_cov16 (16x16x4 tiles: 36 of 64 upper tiles at d = 128;
  *                       7.35 vs 7.92 ms at C4); 1: k_gmm_cov_async (32x32 tiles, 2 image
  *                       buffers, 2 workgroups per CU); 2 = its 3-buffer form (1 workgroup per

@@ -424,6 +424,172 @@ __global__ void __launch_bounds__(256, 2) k_community_async(CommArgs a) {
     }
 }
 
+// ---- community gradient on 16x16x4 MFMAs, one 16-row tile per wavefront (community_async = 2) --
+//
+// k_community_async's staging (two half images of M_k = Sigma_k^-1, set A = columns s < D/2 and
+// set B = the rest, each half staged while the other is multiplied; mu_k double-buffered), with
+// the E-step's wave shape: 8 wavefronts x 16 rows per 128-row workgroup, about 90 VGPRs, so the
+// two workgroups the LDS holds per CU give 4 waves per SIMD instead of 2.  MFMA (column tile ct,
+// feature quad q; 4 k-steps t): A[i][k] = M_k[16 ct + i][16 q + 4 k + t] (one ds_read_b128 of
+// the swizzled half image per block), B[k][j] = pi_jk (x_j - mu_k)[16 q + 4 k + t] (registers:
+// the lane's row j = lane % 16 holds features 16 q + 4 (lane / 16) .. + 3 of every quad), so the
+// output D[i][j] = G[row j][16 ct + i] lands in the layout x is held in: the update x -= lr *
+// clip(coef G, -5, 5) happens in registers.  pi[row, k + 1] is prefetched into a register during
+// component k.
+template <int D>
+struct Comm16 {
+    static constexpr int NQ = D / 16;               // feature quads = column tiles
+    static constexpr int RL = D / 8;                // 16-B granules per half-image row
+    static constexpr int RPB = 16 / RL;             // rows per 256-B bank row
+    static constexpr int SET = D * D / 2;           // floats per half image
+    static constexpr int MUS = D * D;               // 2 x 256 floats: mu_k, double-buffered (a
+                                                    // 64-lane copy writes 256 floats)
+    static constexpr int LDS_FLOATS = D * D + 512;
+    static constexpr int NW = 8;                    // wavefronts per workgroup
+    // float offset of (row c, logical granule g of the full row) in half image g / RL
+    __host__ __device__ static constexpr int at(int c, int g) {
+        return (g / RL) * SET + c * RL * 4 + (((g % RL) ^ ((c / RPB) & (RL - 1))) * 4);
+    }
+};
+
+// Piece i (1 KiB = ROWS rows) of half image SETI, i = wid + NW j: lane l fills row c = ROWS i + l / RL,
+// physical granule l % RL, from the logical granule the swizzle puts there.  The swizzle key of
+// c is the same for every j of a wavefront (NW ROWS / RPB is a multiple of RL), so one lane offset
+// serves all its pieces.
+template <int D, int SETI>
+__device__ __forceinline__ void comm16_stage_set(const float *Mk, float *sm, int wid, int lane) {
+    using C = Comm16<D>;
+    constexpr int PIECES = C::SET / 256;
+    constexpr int ROWS = 256 / (C::RL * 4);  // rows per 1 KiB piece
+    static_assert((C::NW * ROWS / C::RPB) % C::RL == 0, "one swizzle key per wavefront");
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // recompute the offsets per call: hoisted, they cost 16 VGPRs
+    const int c0 = wid * ROWS + ln / C::RL, pg = ln % C::RL;
+    // bytes from a wavefront-uniform base: the saddr form, one VGPR for every piece
+    const uint32_t loff =
+        4u * (uint32_t)(c0 * D + 4 * (SETI * C::RL + (pg ^ ((c0 / C::RPB) & (C::RL - 1)))));
+#pragma unroll
+    for (int j = 0; j < (PIECES + C::NW - 1) / C::NW; ++j) {
+        const int i = wid + C::NW * j;
+        if (i >= PIECES) break;  // wavefront-uniform
+        const char *base = reinterpret_cast<const char *>(Mk + j * C::NW * ROWS * D);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const float *>(base + loff),
+                                         sm + SETI * C::SET + i * 256, 16, 0, 0);
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void comm16_stage_mu(const float *mu, float *sm, int buf, int wid,
+                                                int lane) {
+    if (wid == 0) {
+        const int src = lane * 4 < D ? lane * 4 : D - 4;
+        __builtin_amdgcn_global_load_lds(mu + src, sm + Comm16<D>::MUS + buf * 256, 16, 0, 0);
+    }
+}
+
+// the blocks of half H (quads q in [H NQ/2, (H+1) NQ/2), every column tile) into acc
+// abase[a]: the lane's offset (floats) of granule 4 a + kg of its row j16 in column tile 0 of a
+// half image; block (q, ct) adds the compile-time (q / (RL/4)) SET + 16 ct RL 4 (the swizzle depends
+// on the row only through j16).
+template <int D, int H>
+__device__ __forceinline__ void comm16_phase(const __attribute__((ext_vector_type(4))) float (&xb)[D / 16],
+                                             const float *sm, const float *mus, float p,
+                                             const int (&abase)[D / 32], int kg,
+                                             __attribute__((ext_vector_type(4))) float (&acc)[D / 16]) {
+    using C = Comm16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int NQ = C::NQ, HQ = NQ / 2, NB = HQ * NQ;
+    f32x4 bq[HQ];
+#pragma unroll
+    for (int qq = 0; qq < HQ; ++qq) {
+        const int q = H * HQ + qq;
+        const f32x4 m = *reinterpret_cast<const f32x4 *>(mus + 16 * q + 4 * kg);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bq[qq][t] = p * (xb[q][t] - m[t]);
+    }
+    auto fetch = [&](int n) {  // block n = (qq, ct), qq-major
+        const int q = H * HQ + n / NQ, ct = n % NQ;
+        return *reinterpret_cast<const f32x4 *>(sm + (q / (C::RL / 4)) * C::SET +
+                                                ct * 16 * C::RL * 4 + abase[q % (C::RL / 4)]);
+    };
+    f32x4 av[3];
+    av[0] = fetch(0);
+    av[1] = fetch(1);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+        if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
+        const int qq = n / NQ, ct = n % NQ;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], bq[qq][t], acc[ct], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(512, 4) k_community16(CommArgs a) {
+    using C = Comm16<D>;
+    constexpr int NQ = C::NQ;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int j16 = lane & 15, kg = lane >> 4;
+    const int64_t row = (int64_t)blockIdx.x * 128 + wid * 16 + j16;
+    const bool rowok = row < a.V;
+    f32x4 xb[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+        xb[q] = rowok ? *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg)
+                      : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    int abase[C::RL / 4];
+#pragma unroll
+    for (int q4 = 0; q4 < C::RL / 4; ++q4)
+        abase[q4] = j16 * C::RL * 4 + 4 * ((4 * q4 + kg) ^ ((j16 / C::RPB) & (C::RL - 1)));
+    for (int it = 0; it < a.iters; ++it) {
+        __syncthreads();  // the previous iteration's last half image is free
+        comm16_stage_set<D, 0>(a.inv_cov, sm, wid, lane);
+        comm16_stage_set<D, 1>(a.inv_cov, sm, wid, lane);
+        comm16_stage_mu<D>(a.mu, sm, 0, wid, lane);
+        float pn = rowok ? a.pi[row * a.K] : 0.0f;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        f32x4 acc[NQ];
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int k = 0; k < a.K; ++k) {
+            const float p = pn;
+            const float *mus = sm + C::MUS + (k & 1) * 256;
+            const float *Mn = a.inv_cov + (int64_t)(k + 1) * D * D;
+            comm16_phase<D, 0>(xb, sm, mus, p, abase, kg, acc);  // set A of M_k
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // set A free; set B of M_k in LDS
+            if (k + 1 < a.K) {
+                comm16_stage_set<D, 0>(Mn, sm, wid, lane);
+                comm16_stage_mu<D>(a.mu + (int64_t)(k + 1) * D, sm, (k + 1) & 1, wid, lane);
+                pn = rowok ? a.pi[row * a.K + k + 1] : 0.0f;
+            }
+            comm16_phase<D, 1>(xb, sm, mus, p, abase, kg, acc);  // set B of M_k
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // set B free; set A and mu of k + 1 in LDS
+            if (k + 1 < a.K) comm16_stage_set<D, 1>(Mn, sm, wid, lane);
+        }
+        // x -= lr * clip(coef * G, -5, 5), in registers (lane: row j16, columns 16 ct + 4 kg + e)
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float g = acc[ct][e] * a.coef;
+                g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);
+                xb[ct][e] = xb[ct][e] - g * a.lr;
+            }
+    }
+    if (rowok) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) *reinterpret_cast<f32x4 *>(a.x + row * D + 16 * q + 4 * kg) = xb[q];
+    }
+}
+
 // GMM responsibilities on MFMA (d in {64, 128}): for each component the tile computes
 // Y = X P_k (A = the rows, B = P_k), then sum_c (Y - mu P_k)^2 per row: squares summed over the CT
 // column tiles in registers, then over the 32 columns of a half-wave with the DPP / permlane16
@@ -2247,6 +2413,23 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     int rc = ensure_init(&dev);
     if (rc) return rc;
     CommArgs a{x, pi, mu, inv_cov, V, d, K, (float)((double)beta / (double)K), lr, iters};
+    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 &&
+        ((uintptr_t)mu % 16) == 0 && current_opts().community_async == 2) {
+        const unsigned grid = (unsigned)((V + 127) / 128);
+        const size_t lds = sizeof(float) * (size_t)(d == 64 ? Comm16<64>::LDS_FLOATS
+                                                            : Comm16<128>::LDS_FLOATS);
+        static bool attr_16 = false;
+        if (!attr_16) {
+            (void)hipFuncSetAttribute((const void *)k_community16<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void *)k_community16<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_16 = true;
+        }
+        hipLaunchKernelGGL(d == 64 ? k_community16<64> : k_community16<128>, dim3(grid), dim3(512),
+                           lds, (hipStream_t)stream, a);
+        return hip_error(hipGetLastError(), "k_community16 launch");
+    }
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 &&
         ((uintptr_t)mu % 16) == 0 && current_opts().community_async) {
         const unsigned grid = (unsigned)((V + 127) / 128);

@@ -370,12 +370,27 @@ def test_community_grad_vs_golden():
 
 
 @pytest.mark.parametrize("d,V,K,iters", [(64, 1000, 7, 3), (128, 777, 5, 2), (128, 300, 1, 1),
-                                          (96, 200, 3, 2), (256, 150, 3, 2), (500, 37, 2, 1)])
-def test_community_grad_vs_oracle(d, V, K, iters):
-    """MFMA path (d = 64, 128; ragged row tiles), VALU path (d = 96) and the wide VALU path
-    (d = 256, 500: matrices streamed in row chunks) against the numpy
-    restatement of community_embeddings.py:61-78: fp32 contractions in another order,
+                                          (96, 200, 3, 2), (256, 150, 3, 2), (500, 37, 2, 1),
+                                          (128, 4097, 4, 2), (64, 129, 3, 1)])
+@pytest.mark.parametrize("kern", [1, 2])
+def test_community_grad_vs_oracle(d, V, K, iters, kern):
+    """MFMA path (d = 64, 128; ragged row tiles; community_async = 1: k_community_async on
+    32x32x2 MFMAs, 2: k_community16 on 16x16x4 with one row tile per wavefront), VALU path
+    (d = 96) and the wide VALU path (d = 256, 500: matrices streamed in row chunks) against the
+    numpy restatement of community_embeddings.py:61-78: fp32 contractions in another order,
     rtol/atol 2e-5; the clip at +-5 is exercised (beta large)."""
+    from come_amd import _lib
+    if kern == 2 and d not in (64, 128):
+        pytest.skip("k_community16 serves d = 64, 128")
+    prev = _lib.launch_opts().community_async
+    _lib.set_option("community_async", kern)
+    try:
+        _community_vs_oracle(d, V, K, iters)
+    finally:
+        _lib.set_option("community_async", prev)
+
+
+def _community_vs_oracle(d, V, K, iters):
     rng = np.random.RandomState(d + V)
     x0 = rng.normal(size=(V, d)).astype(np.float32)
     A = rng.normal(size=(K, d, d)) / np.sqrt(d)
