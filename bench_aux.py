@@ -176,9 +176,10 @@ def c4(args):
     ct16 = d // 16 if d in (64, 128) else 0
     tri_resp = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_resp16 else tri) if ct16 \
         else 1.0
-    tri_cov = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_cov_async == 3 else tri) \
+    tri_cov = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_cov_async in (3, 4) else tri) \
         if ct16 else 1.0
-    cov_kernel = ({3: "k_gmm_cov16", 0: "k_gmm_cov_mfma"}.get(opts.gmm_cov_async, "k_gmm_cov_async")
+    cov_kernel = ({3: "k_gmm_cov16", 4: "k_gmm_cov16<W=1>", 0: "k_gmm_cov_mfma"}.get(
+        opts.gmm_cov_async, "k_gmm_cov_async")
                   if ct16 else "VALU")
     comm_kernel = ({2: "k_community16", 0: "k_community_mfma"}.get(opts.community_async,
                                                                    "k_community_async")

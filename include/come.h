@@ -254,7 +254,8 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *   gmm_cov_async       default 3: k_gmm_cov16 (16x16x4 tiles: 36 of 64 upper tiles at d = 128;
  *                       7.35 vs 7.92 ms at C4); 1: k_gmm_cov_async (32x32 tiles, 2 image
  *                       buffers, 2 workgroups per CU); 2 = its 3-buffer form (1 workgroup per
- *                       CU); 0 = k_gmm_cov_mfma
+ *                       CU); 4 = k_gmm_cov16 with each component's tiles over 4 MFMA
+ *                       wavefronts (bit-identical to 3; 7.45 ms, no gain); 0 = k_gmm_cov_mfma
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)

@@ -1998,7 +1998,10 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
 // conflict-free without padding).  A d = 128 component's 36 tiles split 18 / 18 over two
 // wavefronts by tile rows {0, 1, 6, 7} and {2, 3, 4, 5}; a wavefront weights its 4 A rows once
 // per group and streams the B rows column by column (few VGPRs at 4 waves per SIMD).
-template <int D>
+// W = 1 (gmm_cov_async = 4): twice the MFMA wavefronts, each with half the tiles (tile rows
+// {p, NT16 - 1 - p}: 9 tiles at d = 128, 5 at 64), so 8 MFMA + 4 staging wavefronts per workgroup
+// and 4 MFMA waves per SIMD instead of 2 (the E-step / community lesson).
+template <int D, int W = 0>
 struct Cov16 {
     static constexpr int RB = 32;                 // samples per block
     static constexpr int LDT = RB;                // image row (swizzled, unpadded)
@@ -2008,22 +2011,25 @@ struct Cov16 {
     static constexpr int BUF = CPW * IMG + CPW * RB;
     static constexpr int NBUF = 2;
     static constexpr int NT16 = D / 16;
-    static constexpr int WPC = D == 128 ? 2 : 1;  // MFMA wavefronts per component
-    static constexpr int NTW = NT16 * (NT16 + 1) / 2 / WPC;  // tiles per wavefront
-    static constexpr int NR = 4;                  // A rows per wavefront
+    static constexpr int WPC = (D == 128 ? 2 : 1) * (W ? 2 : 1);  // MFMA wavefronts per component
+    static constexpr int NTW = NT16 * (NT16 + 1) / 2 / WPC;      // tiles per wavefront
+    static constexpr int NR = W ? 2 : 4;                          // A rows per wavefront
+    static constexpr int AW = CPW * WPC;                          // MFMA wavefronts
+    static constexpr int THREADS = 64 * (AW + 4);                 // + 4 staging wavefronts
 };
 
-// Tiles of MFMA wavefront part p (0 / 1 at d = 128; 0 at d = 64) in issue order (column-major:
-// B row ct once per column), with their A-row slot.
-template <int D>
+// Tiles of MFMA wavefront part p (W = 0: 0 / 1 at d = 128, 0 at d = 64) in issue order
+// (column-major: B row ct once per column), with their A-row slot.
+template <int D, int W = 0>
 struct Cov16Tiles {
-    using C = Cov16<D>;
-    int rows[2][C::NR];
-    int ct[2][C::NTW], slot[2][C::NTW];
+    using C = Cov16<D, W>;
+    int rows[C::WPC][C::NR];
+    int ct[C::WPC][C::NTW], slot[C::WPC][C::NTW];
     constexpr Cov16Tiles() : rows(), ct(), slot() {
         for (int p = 0; p < C::WPC; ++p) {
             for (int i = 0; i < C::NR; ++i)
-                rows[p][i] = D == 64 ? i : (p == 0 ? (i < 2 ? i : i + 4) : i + 2);
+                rows[p][i] = W ? (i == 0 ? p : C::NT16 - 1 - p)
+                               : (D == 64 ? i : (p == 0 ? (i < 2 ? i : i + 4) : i + 2));
             int n = 0;
             for (int c = 0; c < C::NT16; ++c)
                 for (int i = 0; i < C::NR; ++i)
@@ -2041,13 +2047,13 @@ __device__ __forceinline__ int cov16_off(int c, int gran) {  // image offset of 
     return c * Cov16<D>::LDT + 4 * (gran ^ (c & 7));
 }
 
-template <int D, int P>
+template <int D, int W, int P>
 __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, int lane,
                                               __attribute__((ext_vector_type(4)))
-                                              float (&acc)[Cov16<D>::NTW]) {
-    using C = Cov16<D>;
+                                              float (&acc)[Cov16<D, W>::NTW]) {
+    using C = Cov16<D, W>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr Cov16Tiles<D> TT{};
+    constexpr Cov16Tiles<D, W> TT{};
     const int j16 = lane & 15, kg = lane >> 4;
     for (int j = 0; j < nb; ++j) {
         __syncthreads();  // barrier j: block j staged
@@ -2081,12 +2087,39 @@ __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, 
     }
 }
 
-template <int D>
-__global__ void __launch_bounds__(CovShape<D>::ATHREADS)
-    __attribute__((amdgpu_waves_per_eu(4))) k_gmm_cov16(CovArgs a) {
-    using C = Cov16<D>;
+// the MFMA part of wavefront part P (compile-time tile tables): consume, then store the tiles
+template <int D, int W, int P>
+__device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, int nb, int tk,
+                                           int nk, int k0, int lane) {
+    using C = Cov16<D, W>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    f32x4 acc[C::NTW];
+#pragma unroll
+    for (int n = 0; n < C::NTW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (nb > 0) cov16_consume<D, W, P>(img, nb, tk, lane, acc);
+    if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+    constexpr Cov16Tiles<D, W> TT{};
+    const int j16 = lane & 15, kg = lane >> 4;
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
+#pragma unroll
+    for (int n = 0; n < C::NTW; ++n) {
+        const int rt = TT.rows[P][TT.slot[P][n]], ct = TT.ct[P][n];
+        const int jj = ct * 16 + j16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int ii = rt * 16 + 4 * kg + e;
+            out[(int64_t)ii * D + jj] = acc[n][e];
+            if (rt != ct) out[(int64_t)jj * D + ii] = acc[n][e];
+        }
+    }
+}
+
+template <int D, int W>
+__global__ void __launch_bounds__((Cov16<D, W>::THREADS))
+    __attribute__((amdgpu_waves_per_eu(W ? 6 : 4))) k_gmm_cov16(CovArgs a) {
+    using C = Cov16<D, W>;
     constexpr int CPW = C::CPW;
-    constexpr int NST = 64 * CovShape<D>::AWAVES;  // staging threads
+    constexpr int NST = 256;  // staging threads (4 wavefronts)
     constexpr int RB = C::RB;
     constexpr int SPT = RB * D / NST;  // samples staged per thread (16 at d = 128, 8 at d = 64)
     using f32x4 = __attribute__((ext_vector_type(4))) float;
@@ -2100,43 +2133,25 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
     if (c1 > a.V) c1 = a.V;
     const int nb = c1 > c0 ? (int)((c1 - c0 + RB - 1) / RB) : 0;
     const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    if (wid < CovShape<D>::AWAVES) {
+    if (wid < C::AW) {
         // ---- MFMA wavefronts: component tk, tile part p ----
         const int tk = wid / C::WPC, p = wid % C::WPC;
-        f32x4 acc[C::NTW];
-#pragma unroll
-        for (int n = 0; n < C::NTW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (nb > 0) {
-            if (p == 0) cov16_consume<D, 0>(img, nb, tk, lane, acc);
-            else cov16_consume<D, (C::WPC > 1 ? 1 : 0)>(img, nb, tk, lane, acc);
-        }
-        if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
-        constexpr Cov16Tiles<D> TT{};
-        const int j16 = lane & 15, kg = lane >> 4;
-        float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
-#pragma unroll
-        for (int n = 0; n < C::NTW; ++n) {
-            const int rt = p == 0 ? TT.rows[0][TT.slot[0][n]] : TT.rows[C::WPC - 1][TT.slot[C::WPC - 1][n]];
-            const int ct = p == 0 ? TT.ct[0][n] : TT.ct[C::WPC - 1][n];
-            const int jj = ct * 16 + j16;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int ii = rt * 16 + 4 * kg + e;
-                out[(int64_t)ii * D + jj] = acc[n][e];
-                if (rt != ct) out[(int64_t)jj * D + ii] = acc[n][e];
-            }
-        }
+        constexpr int P1 = C::WPC > 1 ? 1 : 0, P2 = C::WPC > 2 ? 2 : 0, P3 = C::WPC > 3 ? 3 : 0;
+        if (p == 0) cov16_part<D, W, 0>(a, img, nb, tk, nk, k0, lane);
+        else if (p == 1) cov16_part<D, W, P1>(a, img, nb, tk, nk, k0, lane);
+        else if (p == 2) cov16_part<D, W, P2>(a, img, nb, tk, nk, k0, lane);
+        else cov16_part<D, W, P3>(a, img, nb, tk, nk, k0, lane);
         return;
     }
     // ---- staging wavefronts (as k_gmm_cov_async): thread owns column sc and samples SPT sp ..
     // SPT sp + SPT - 1 of a block; lane l < SPT * CPW also carries one weight ----
-    const int st = tid - NST;
+    const int st = tid - 64 * C::AW;
     const int sc = st % D, sp = st / D;
     float mu[CPW];
 #pragma unroll
     for (int kk = 0; kk < CPW; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
-    float xv[3][SPT];
-    float wl[3];
+    float xv[W ? 2 : 3][SPT];
+    float wl[W ? 2 : 3];
     const int wk = lane / SPT, ws = lane % SPT;
     const bool wlane = lane < SPT * CPW;
     auto load = [&](int blk, float (&xr)[SPT], float &wr) {
@@ -2168,24 +2183,46 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
     };
     if (nb == 0) return;
     constexpr int SD = C::NBUF - 1;  // block j + 1 is staged while block j is multiplied
+    if constexpr (W == 0) {
 #pragma unroll
-    for (int u = 0; u < 3; ++u)
-        if (u < nb) load(u, xv[u], wl[u]);
-    if (0 < nb) {
-        stage(0, xv[0], wl[0]);
-        if (3 < nb) load(3, xv[0], wl[0]);
-    }
-    __syncthreads();  // barrier 0
-    for (int j0 = 0; j0 < nb; j0 += 3) {
+        for (int u = 0; u < 3; ++u)
+            if (u < nb) load(u, xv[u], wl[u]);
+        if (0 < nb) {
+            stage(0, xv[0], wl[0]);
+            if (3 < nb) load(3, xv[0], wl[0]);
+        }
+        __syncthreads();  // barrier 0
+        for (int j0 = 0; j0 < nb; j0 += 3) {
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
-            const int j = j0 + u;
-            if (j >= nb) break;
-            if (j + SD < nb) {
-                stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-                if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+            for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
+                const int j = j0 + u;
+                if (j >= nb) break;
+                if (j + SD < nb) {
+                    stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+                    if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+                }
+                if (j + 1 < nb) __syncthreads();  // barrier j + 1
             }
-            if (j + 1 < nb) __syncthreads();  // barrier j + 1
+        }
+    } else {
+        // two register sets (the registers 6 waves per SIMD allow): block b lives in set b % 2,
+        // loaded two blocks before it is staged
+        load(0, xv[0], wl[0]);
+        if (1 < nb) load(1, xv[1], wl[1]);
+        stage(0, xv[0], wl[0]);
+        if (2 < nb) load(2, xv[0], wl[0]);
+        __syncthreads();  // barrier 0
+        for (int j0 = 0; j0 < nb; j0 += 2) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {  // j = j0 + u: block j + 1 in set (u + 1) % 2
+                const int j = j0 + u;
+                if (j >= nb) break;
+                if (j + 1 < nb) {
+                    stage(j + 1, xv[(u + 1) % 2], wl[(u + 1) % 2]);
+                    if (j + 3 < nb) load(j + 3, xv[(u + 1) % 2], wl[(u + 1) % 2]);
+                }
+                if (j + 1 < nb) __syncthreads();  // barrier j + 1
+            }
         }
     }
 }
@@ -2693,16 +2730,20 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
     const bool cov_async = current_opts().gmm_cov_async != 0;
-    const bool cov16 = mfma && current_opts().gmm_cov_async == 3;
+    const int cov16 = mfma && current_opts().gmm_cov_async == 3   ? 1
+                      : mfma && current_opts().gmm_cov_async == 4 ? 2
+                                                                   : 0;
     void (*kern)(CovArgs) =
         !mfma ? k_gmm_cov_valu
-              : cov16 ? (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>)
+              : cov16 == 2 ? (d == 64 ? k_gmm_cov16<64, 1> : k_gmm_cov16<128, 1>)
+              : cov16 ? (d == 64 ? k_gmm_cov16<64, 0> : k_gmm_cov16<128, 0>)
               : cov_async ? (current_opts().gmm_cov_async == 2
                                  ? (d == 64 ? k_gmm_cov_async<64, 3> : k_gmm_cov_async<128, 3>)
                                  : (d == 64 ? k_gmm_cov_async<64, 2> : k_gmm_cov_async<128, 2>))
                             : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
-    const int threads = !mfma      ? 256
-                        : cov_async ? CovShape<128>::ATHREADS
+    const int threads = !mfma        ? 256
+                        : cov16 == 2 ? (d == 64 ? Cov16<64, 1>::THREADS : Cov16<128, 1>::THREADS)
+                        : cov_async  ? CovShape<128>::ATHREADS
                                     : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
     const int cpw = !mfma || !cov_async ? 1
                     : cov16      ? (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW)

@@ -147,7 +147,7 @@ def test_estep16t_variants_bit_identical(V, K, d):
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
                                           (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None),
                                           (1500, 3, 256, 4), (200, 2, 330, None)])
-@pytest.mark.parametrize("cov", [1, 3])
+@pytest.mark.parametrize("cov", [1, 3, 4])
 def test_scatter_vs_numpy(V, K, d, chunks, cov):
     rng = np.random.RandomState(V + K)
     X = rng.normal(size=(V, d)).astype(np.float32)
@@ -248,7 +248,8 @@ def test_community2vec_distributed_flag_single_process_matches():
 def test_scatter_async_matches_sync(V, K, d, chunks):
     """k_gmm_cov_async (2 (d=128) / 4 (d=64) components per workgroup, operands centred and
     weighted once per block into transposed LDS images, the same fp32 products) and k_gmm_cov16
-    (the same on 16x16x4 tiles, gmm_cov_async = 3) against the synchronous k_gmm_cov_mfma: equal
+    (the same on 16x16x4 tiles, gmm_cov_async = 3; 4: its tiles over twice the wavefronts, bit-
+    identical to 3) against the synchronous k_gmm_cov_mfma: equal
     up to the order the MFMAs accumulate the samples in (atol 1e-5 of the matrix scale).  K not a
     multiple of the components per workgroup included."""
     from come_amd import _lib
@@ -258,11 +259,12 @@ def test_scatter_async_matches_sync(V, K, d, chunks):
     resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
     mu = t(rng.standard_normal((K, d)).astype(np.float32))
     out = []
-    for opt in (0, 1, 2, 3):  # sync; async with 2 image buffers / with 3; 16x16x4 tiles
-        with opts(gmm_cov_async=opt):
+    for opt in (0, 1, 2, 3, 4):  # sync; async with 2 image buffers / with 3; 16x16x4 tiles;
+        with opts(gmm_cov_async=opt):  # 16x16x4 with twice the MFMA wavefronts
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
     for o in out[1:]:
         np.testing.assert_allclose(o, out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
+    np.testing.assert_array_equal(out[4], out[3])  # the same per-tile sample order
 
 
 def test_community2vec_trains_at_d256():
