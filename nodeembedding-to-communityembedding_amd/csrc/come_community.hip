@@ -1444,13 +1444,31 @@ __device__ __forceinline__ float r16t_lp(
     using f32x2 = __attribute__((ext_vector_type(2))) float;
     const float lnk = buf[T::PAR + 1];
     f32x4 acc[RT][NQ];
+    if constexpr ((VT & 32) != 0) {  // accumulators start at -mu_k P_k (own rounding)
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+        for (int ct = 0; ct < NQ; ++ct) {
+            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
 #pragma unroll
-        for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int rt = 0; rt < RT; ++rt) acc[rt][ct] = -mp;
+        }
+    } else {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
     r16t_blocks<D, VT>(xb, buf, abase, acc, after_first);
     float sq[RT];
-    if constexpr ((VT & 2) == 0) {
+    if constexpr ((VT & 32) != 0) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) sq[rt] = 0.0f;
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sq[rt] = __builtin_fmaf(acc[rt][ct][e], acc[rt][ct][e], sq[rt]);
+    } else if constexpr ((VT & 2) == 0) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) sq[rt] = 0.0f;
 #pragma unroll
@@ -1542,12 +1560,16 @@ __device__ __forceinline__ void r16t_body(const RespArgs &a, float *sm) {
             if constexpr ((VT & 4) != 0) stage_next();
         });
         if (owner) a.resp[my_row * a.K + k] = lp;
-        lse_push(lp, run_max, run_sum);
+        if constexpr ((VT & 16) == 0) lse_push(lp, run_max, run_sum);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
     }
     if (owner) {
         float *lp = a.resp + my_row * a.K;
+        if constexpr ((VT & 16) != 0) {  // VT & 16: the log-sum-exp after the loop (max first)
+            for (int k = 0; k < a.K; ++k) run_max = fmaxf(run_max, lp[k]);
+            for (int k = 0; k < a.K; ++k) run_sum += expf(lp[k] - run_max);
+        }
         const float lse = run_max + logf(run_sum);
         for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
         if (a.lse) a.lse[my_row] = lse;
@@ -2568,13 +2590,18 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         // 8 = one row tile (the default: 7.00 vs 7.10 ms at C4, bit-identical to 0), 10 = one row
         // tile + packed epilogue (7.01 ms; profiles/r04_ab_estep16.txt; 10-wavefront workgroups
         // of VT 8: 8.7 ms).  gmm_resp16 = 2: VT 8; 16 + i: entry i (A/B)
-        static const int kVts[4] = {0, 2, 8, 10};
-        static void (*const k_r16t[4][2])(RespArgs) = {
+        // (A/B, late round 3: 24 = 8 with the log-sum-exp after the loop, 40 = 8 with the
+        // accumulators started at -mu_k P_k, 56 = both: gmm_resp16 = 20, 21, 22)
+        static const int kVts[7] = {0, 2, 8, 10, 24, 40, 56};
+        static void (*const k_r16t[7][2])(RespArgs) = {
             {k_gmm_resp16t<64, 0>, k_gmm_resp16t<128, 0>},
             {k_gmm_resp16t<64, 2>, k_gmm_resp16t<128, 2>},
             {k_gmm_resp16t<64, 8>, k_gmm_resp16t<128, 8>},
-            {k_gmm_resp16t<64, 10>, k_gmm_resp16t<128, 10>}};
-        if (r16 == 2 || (r16 >= 16 && r16 < 20)) {
+            {k_gmm_resp16t<64, 10>, k_gmm_resp16t<128, 10>},
+            {k_gmm_resp16t<64, 24>, k_gmm_resp16t<128, 24>},
+            {k_gmm_resp16t<64, 40>, k_gmm_resp16t<128, 40>},
+            {k_gmm_resp16t<64, 56>, k_gmm_resp16t<128, 56>}};
+        if (r16 == 2 || (r16 >= 16 && r16 < 23)) {
             const int tri = d == 64 ? Resp16T<64>::TRI : Resp16T<128>::TRI;
             float *packed = stream_scratch(dev, stream, kScratchGmmTri, sizeof(float) * (size_t)K * tri);
             if (!packed) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
@@ -2591,7 +2618,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
                 d == 64 ? Resp16Shape<64>::LDS : Resp16Shape<128>::LDS);
             static bool attr16t = false;
             if (!attr16t) {
-                for (int v = 0; v < 4; ++v)
+                for (int v = 0; v < 7; ++v)
                     for (int dd = 0; dd < 2; ++dd)
                         (void)hipFuncSetAttribute((const void *)k_r16t[v][dd],
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
