@@ -11,6 +11,27 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_gmm.py -m gpu -v -k "estep"
 PYTEST_RC=$?
 grep -E "FAILED|passed|failed|Error" gpurun_out/r04z_pytest.log | tail -12
 [ $PYTEST_RC -eq 0 ] || exit $PYTEST_RC
+timeout -k 10 120 python - <<'PY' || exit 1
+import numpy as np, torch
+from come_amd import _lib, gmm
+rng = np.random.RandomState(5)
+for V, K, d in ((4097, 50, 128), (3001, 7, 64)):
+    X = rng.standard_normal((V, d)).astype(np.float32)
+    P = np.stack([np.triu(rng.standard_normal((d, d)) / np.sqrt(d)) + 2 * np.eye(d) for _ in range(K)])
+    mp = np.einsum("kd,kde->ke", rng.standard_normal((K, d)) * 0.3, P)
+    ln = np.log(rng.dirichlet(np.ones(K)))
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device="cuda")
+    out = {}
+    for r in (2, 20, 21, 22):
+        _lib.set_option("gmm_resp16", r)
+        resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
+        out[r] = resp.cpu().numpy(), lse.cpu().numpy()
+    _lib.set_option("gmm_resp16", 2)
+    for r in (20, 21, 22):
+        dr = np.abs(out[r][0] - out[2][0]).max(); dl = np.abs(out[r][1] - out[2][1]).max()
+        print("variant", r, "d", d, "max |resp diff|", dr, "max |lse diff|", dl)
+        assert dr < 1e-4 and dl < 1e-3
+PY
 # E-step epilogue variants: 20 = log-sum-exp after the loop, 21 = accumulators from -mu P, 22 = both
 for P in 1 2; do
 for R in 2 20 21 22; do
