@@ -167,26 +167,21 @@ def c4(args):
                                     orc.precision_cholesky(cov), dev)
     flops = 2.0 * V * K * d * d
     # fraction of the MFMA blocks executed on sklearn's upper-triangular precision factors: the
-    # E-step's 16-wide blocks (k_gmm_resp16, 36 of 64 at d = 128) or 32-wide ones
-    # (k_gmm_resp_mfma / _db, 10 of 16); the scatter's symmetric 32-wide tiles (10 of 16)
+    # E-step's 16-wide blocks (k_gmm_resp16t, 36 of 64 at d = 128) or the fallback's 32-wide ones
+    # (k_gmm_resp_mfma, 10 of 16); the scatter's symmetric 16-wide (36 of 64) / 32-wide tiles
     from come_amd import _lib
     opts = _lib.launch_opts()
     ct = d // 32 if d in (64, 128) else 0
     tri = (ct * (ct + 1) / 2) / (ct * ct) if ct else 1.0
     ct16 = d // 16 if d in (64, 128) else 0
-    tri_resp = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_resp16 else tri) if ct16 \
-        else 1.0
-    tri_cov = ((ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if opts.gmm_cov_async in (3, 4) else tri) \
-        if ct16 else 1.0
-    cov_kernel = ({3: "k_gmm_cov16", 4: "k_gmm_cov16<W=1>", 0: "k_gmm_cov_mfma"}.get(
-        opts.gmm_cov_async, "k_gmm_cov_async")
-                  if ct16 else "VALU")
-    comm_kernel = ({2: "k_community16", 0: "k_community_mfma"}.get(opts.community_async,
-                                                                   "k_community_async")
-                   if ct16 else "VALU")
-    resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 or 16 <= opts.gmm_resp16 < 20
-                   else "k_gmm_resp16" if opts.gmm_resp16
-                   else "k_gmm_resp_db" if opts.gmm_resp_db else "k_gmm_resp_mfma") if ct16 \
+    tri16 = (ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if ct16 else 1.0
+    tri_resp = (tri16 if opts.gmm_resp16 == 2 else tri) if ct16 else 1.0
+    tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
+    cov_kernel = ("k_gmm_cov16" if opts.gmm_cov_async == 3 else "k_gmm_cov_async") if ct16 \
+        else "VALU"
+    comm_kernel = ("k_community16" if opts.community_async == 2 else "k_community_async") \
+        if ct16 else "VALU"
+    resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp_mfma") if ct16 \
         else "VALU"
     x0 = x.clone()
     xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]

@@ -33,11 +33,14 @@
 extern "C" {
 #endif
 
-/* ABI 2 (this header): come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
+/* ABI 3 (this header): the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B
+ * kernels) was removed, "community_async" accepts 1 / 2, "gmm_cov_async" 1 / 3 and "gmm_resp16"
+ * 0 / 2 (other values: COME_E_INVALID at the call); come_source_sha256 was added.
+ * ABI 2: come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
  * options "o2_plain_writeback" and "o2_pair_atomics" (ABI 1, ring-kernel Hogwild) were removed and
  * come_set_option rejects them; o2_kernel = 2 with COME_MODE_HOGWILD returns COME_E_INVALID. */
-#define COME_ABI_VERSION 2
+#define COME_ABI_VERSION 3
 
 enum {
     COME_OK = 0,
@@ -67,6 +70,11 @@ enum {
 #define COME_DEFAULT_HOT_SHARE 5e-6
 
 int come_abi_version(void);
+
+/* SHA-256 (hex) of the sources the library was built from (the csrc .hip / .cpp / .h files, the Makefile
+ * and this header, concatenated in name order): the Python binding refuses a library whose stamp
+ * differs from the sources beside it. */
+const char *come_source_sha256(void);
 const char *come_last_error(void);
 
 /* Uploads the sigmoid table (pyx:531-533) to `device`'s constant memory.  Called implicitly by the
@@ -248,33 +256,24 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *   max_waves           absolute cap on wavefronts in flight (0 = none)
  *   o1_blocks_per_cu    O1 grid cap in 4-wave workgroups per CU (0 = 6)
  *   resident_cap        1 = also clamp grids to the workgroups the occupancy API reports resident
- *   community_async     default 2: k_community16 (16x16x4 MFMAs, one 16-row tile per
- *                       wavefront, 4 waves per SIMD; 11.57 vs 12.46 ms at C4); 1: k_community_async
- *                       (32x32x2, 2 waves per SIMD); 0 = synchronous-staging k_community_mfma
- *   gmm_cov_async       default 3: k_gmm_cov16 (16x16x4 tiles: 36 of 64 upper tiles at d = 128;
- *                       7.35 vs 7.92 ms at C4); 1: k_gmm_cov_async (32x32 tiles, 2 image
- *                       buffers, 2 workgroups per CU); 2 = its 3-buffer form (1 workgroup per
- *                       CU); 4 = k_gmm_cov16 with each component's tiles over 4 MFMA
- *                       wavefronts (bit-identical to 3; 7.45 ms, no gain); 0 = k_gmm_cov_mfma
+ *   community_async     community gradient at d = 64, 128 (16-B aligned mu / inv_cov; else the
+ *                       VALU kernel): default 2 = k_community16 (16x16x4 MFMAs, one 16-row tile
+ *                       per wavefront, 4 waves per SIMD; 11.57 vs 12.46 ms at C4); 1 = the 32x32x2
+ *                       fallback k_community_async.  Other values: COME_E_INVALID
+ *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 3 = k_gmm_cov16 (16x16x4
+ *                       tiles: 36 of 64 upper tiles at d = 128; 7.35 vs 7.92 ms at C4); 1 = the
+ *                       32x32 fallback k_gmm_cov_async.  Other values: COME_E_INVALID
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
  *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
- *   gmm_resp_db         with gmm_resp16 = 0, the 32x32x2 E-step at d = 64, 128: 0 = k_gmm_resp_mfma;
- *                       1 = the double-buffered 8-wavefront kernel (k_gmm_resp_db); 2 = the same
- *                       with the second wave of each SIMD one epilogue late (both bit-identical
- *                       to 0); 3 = 2 with the accumulators started at -mu_k P_k (own rounding);
- *                       other values: COME_E_INVALID at the call
- *   gmm_resp16          GMM E-step at d = 64, 128 on 16x16x4 MFMAs (16-wide triangular skip,
- *                       in-lane row sums): default 2 = k_gmm_resp16t (the factors' non-zero
- *                       16x16 blocks packed, whole components double-buffered, one barrier per
- *                       component; one 16-row tile per wavefront, 8 per workgroup; a launch
- *                       holding a lower or dense factor runs every block, in k_gmm_resp16_full);
- *                       16 + i = k_gmm_resp16t variant i (A/B: 16 two row tiles per wavefront,
- *                       bit-identical to 2; 17 = 16 with a packed-fp32 epilogue; 18 = 2;
- *                       19 = 2 with the packed epilogue); 1 = k_gmm_resp16 (balanced half
- *                       images, two barriers per component); 0 = the 32x32x2 kernels of
- *                       gmm_resp_db.  2 / 16 / 1 / 0: 7.00 / 7.10 / 7.24 / 8.25 ms at C4
+ *   gmm_resp16          GMM E-step at d = 64, 128: default 2 = k_gmm_resp16t on 16x16x4 MFMAs
+ *                       (16-wide triangular skip, in-lane row sums, the factors' non-zero 16x16
+ *                       blocks packed, whole components double-buffered, one barrier per
+ *                       component, one 16-row tile per wavefront; a launch holding a lower or
+ *                       dense factor runs every block, in k_gmm_resp16_full); 0 = the 32x32x2
+ *                       fallback k_gmm_resp_mfma.  7.00 / 8.25 ms at C4.  Other values:
+ *                       COME_E_INVALID
  *   o1_chunk            O1: > 0 = one wavefront per chunk of that many consecutive edges, the
  *                       input row held in registers over each run of edges sharing it
  *                       (k_sgns_o1_runs); default -1 = one contiguous chunk per wavefront of the
@@ -300,7 +299,6 @@ typedef struct come_launch_opts {
     int walk_staged;
     int o2_fresh_loads;
     int o2_atomic_writeback;
-    int gmm_resp_db;
     int gmm_resp16;
     int o1_chunk;
     uint64_t *o2_update_count;
@@ -314,15 +312,21 @@ int come_get_options(come_launch_opts *out);
 int come_set_option(const char *name, int value);
 
 /* come_sgns_o2 with the contended-row bitmap and per-call options.
- * hot_rows  device uint32 [ceil(V / 32)] (come_hot_rows), or NULL: in COME_MODE_HOGWILD the rows
- *           whose bit is set are read right before each pair and updated with float-atomic
- *           deltas at the memory side (no concurrent update lost, no stale cached copy); the
- *           other rows are written back with plain stores.  Ignored in COME_MODE_SEQUENTIAL.
- *           NULL: the library derives the bitmap from `table` on `stream` before the launch
- *           (rows holding >= COME_DEFAULT_HOT_SHARE of the table, ~0.1 ms at T = 1e8, into
- *           library scratch: the first call at a new V allocates, so warm up before capturing a
- *           stream); pass the bitmap to skip that, or COME_HOT_NONE in `mode` for all-cold (on
- *           graphs with hubs that trains measurably worse than the reference's Hogwild,
+ * hot_rows  device uint32 [ceil(V / 32)] (come_hot_rows), or NULL: in COME_MODE_HOGWILD every
+ *           update of a row whose bit is set is a float-atomic delta at the memory side (no
+ *           concurrent update lost); O2 also re-reads such a row before each pair (no stale
+ *           cached copy), while O1's run kernel (o1_chunk != 0) holds its input row -- hot or
+ *           not -- over a run of consecutive edges sharing it and flushes the run's delta once
+ *           (atomically when hot: other wavefronts' updates of the row during the run are kept,
+ *           the run computes on its own copy).  The other rows are written back with plain
+ *           stores.  Ignored in COME_MODE_SEQUENTIAL.
+ *           NULL: the library derives the bitmap from `table` on `stream` before EVERY launch
+ *           (rows holding >= COME_DEFAULT_HOT_SHARE of the table: a memset of V counters and a
+ *           scan of the table, ~0.1 ms at T = 1e8, into library scratch that grows
+ *           stream-ordered -- the first call at a larger V allocates, so warm up before capturing
+ *           a stream).  Callers that launch many small batches should compute the bitmap once
+ *           (come_hot_rows) and pass it; COME_HOT_NONE in `mode` makes every row cold (on graphs
+ *           with hubs that trains measurably worse than the reference's Hogwild,
  *           tests/test_gpu_tierc.py).
  * opts      per-call launch options, or NULL = the process-wide ones. */
 int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const int32_t *walks, int64_t P,

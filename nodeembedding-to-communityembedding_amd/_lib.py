@@ -8,13 +8,14 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # COME_LIB_PATH: an alternative in-tree build of the same library (A/B experiments only)
-LIB_PATH = os.environ.get("COME_LIB_PATH") or os.path.join(HERE, "libcome.so")
+DEFAULT_LIB_PATH = os.path.join(HERE, "libcome.so")
+LIB_PATH = os.environ.get("COME_LIB_PATH") or DEFAULT_LIB_PATH
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
 TABLE_PACKED = 0x100  # COME_TABLE_PACKED mode flag
 HOT_NONE = 0x200      # COME_HOT_NONE mode flag
-ABI_VERSION = 2       # COME_ABI_VERSION this binding is written for
+ABI_VERSION = 3       # COME_ABI_VERSION this binding is written for
 
 # Every symbol include/come.h declares (checked by tests/test_capi.py).
 SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
@@ -27,13 +28,14 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_delta_begin", "come_delta_end", "come_get_options", "come_sgns_o2_ex",
            "come_sgns_o1_ex", "come_hot_rows", "come_lcg_table_draws", "come_delta_flags",
            "come_delta_gather", "come_delta_scatter", "come_cpu_sgns_o2", "come_cpu_sgns_o1",
-           "come_cpu_community_grad", "come_cpu_gmm_resp", "come_cpu_gmm_estep")
+           "come_cpu_community_grad", "come_cpu_gmm_resp", "come_cpu_gmm_estep",
+           "come_source_sha256")
 
 OPTION_FIELDS = ("o2_kernel", "o2_blocks_per_cu", "o2_waves_per_block",
                  "o2_static", "rows_per_wave", "o1_rows_per_wave",
                  "max_waves", "o1_blocks_per_cu", "resident_cap", "community_async",
                  "gmm_cov_async", "walk_staged", "o2_fresh_loads", "o2_atomic_writeback",
-                 "gmm_resp_db", "gmm_resp16", "o1_chunk")
+                 "gmm_resp16", "o1_chunk")
 
 
 class LaunchOpts(ctypes.Structure):
@@ -42,6 +44,22 @@ class LaunchOpts(ctypes.Structure):
                                                              ctypes.c_void_p)]
 
 _lib = None
+
+
+def source_sha256():
+    """SHA-256 of the sources libcome.so is built from, as the Makefile stamps it (csrc/*.hip,
+    *.cpp, *.h in name order, then the Makefile and include/come.h); None without the sources."""
+    import hashlib
+    csrc = os.path.join(HERE, "csrc")
+    header = os.path.join(os.path.dirname(HERE), "include", "come.h")
+    if not os.path.isdir(csrc) or not os.path.exists(header):
+        return None
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".cpp", ".h")))
+    h = hashlib.sha256()
+    for f in [os.path.join(csrc, n) for n in names] + [os.path.join(csrc, "Makefile"), header]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 class ComeError(RuntimeError):
@@ -69,6 +87,7 @@ def lib():
     P, i32, i64, u64, f32, f64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
                                   ctypes.c_float, ctypes.c_double)
     L.come_abi_version.restype = i32
+    L.come_source_sha256.restype = ctypes.c_char_p
     L.come_last_error.restype = ctypes.c_char_p
     L.come_init.argtypes = [i32]
     L.come_exp_table.argtypes = [P]
@@ -114,6 +133,13 @@ def lib():
     if L.come_abi_version() != ABI_VERSION:
         raise ComeError("libcome.so ABI version %d, this binding needs %d (rebuild the library)"
                         % (L.come_abi_version(), ABI_VERSION))
+    want = source_sha256()
+    if want is not None and LIB_PATH == DEFAULT_LIB_PATH:
+        got = L.come_source_sha256().decode()
+        if got != want:
+            raise ComeError("%s was built from other sources (stamp %s, the sources beside it "
+                            "hash to %s): rebuild it with `make -C %s`" % (
+                                LIB_PATH, got[:12], want[:12], os.path.join(HERE, "csrc")))
     _lib = L
     return L
 

@@ -146,121 +146,18 @@ __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
     }
 }
 
-// ---- MFMA version (d in {64, 128}) ------------------------------------------------------
+// ---- MFMA community gradient (d in {64, 128}) ------------------------------------------------
 //
 // G = sum_k A_k M_k^T with A_k[i, :] = pi[i,k] (x_i - mu_k): one GEMM with a reduction of length
-// K*d whose A operand is generated on the fly.  v_mfma_f32_32x32x2_f32 (exact fp32 fmas, 64
-// cycles): lane (r, h) supplies A[row r][j = s + d/2 h] and B[j = s + d/2 h][col r] =
-// M_k[c0 + r][s + d/2 h], so a k-step pairs element s with element s + d/2.  A workgroup of 4
-// wavefronts owns 128 rows (32 per wavefront, CT = d/32 accumulator tiles each); M_k is staged
-// row-major with a 4-float pad (LD = d + 4), read back four k-steps per ds_read_b128.
-// The epilogue moves the tile through LDS (C layout -> rows) to apply the clipped update and to
-// rebuild the A-layout registers for the next iteration.
-template <int D>
-__global__ void __launch_bounds__(256, 2) k_community_mfma(CommArgs a) {
-    constexpr int S = D / 2;  // k-steps per component
-    constexpr int CT = D / 32;
-    constexpr int LD = D + 4;  // 16-B rows: ds_write_b128 staging, ds_read_b128 B operands
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *Ms = sm;             // [D][LD]  (epilogue: [128][LD] row tile)
-    float *mus = sm + 128 * LD;  // [D]
-    const int tid = threadIdx.x;
-    const int wid = tid >> 6, lane = tid & 63;
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t blk0 = (int64_t)blockIdx.x * 128;
-    const int64_t myrow = blk0 + wid * 32 + r;
-    const bool rowok = myrow < a.V;
-    float xa[S];
-#pragma unroll
-    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + q + S * h] : 0.0f;
-
-    for (int it = 0; it < a.iters; ++it) {
-        f32x16 acc[CT];
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-        float p_next = rowok ? a.pi[myrow * a.K] : 0.0f;
-        for (int k = 0; k < a.K; ++k) {
-            __syncthreads();
-            const float *Mk = a.inv_cov + (int64_t)k * D * D;
-            for (int o = tid; o < D * D / 4; o += 256) {
-                const float4 v = reinterpret_cast<const float4 *>(Mk)[o];
-                const int c = (o * 4) / D, j = (o * 4) % D;
-                *reinterpret_cast<float4 *>(Ms + c * LD + j) = v;  // 8-lane groups: 32 banks
-            }
-            if (tid < D) mus[tid] = a.mu[k * D + tid];
-            const float p = p_next;
-            if (k + 1 < a.K) p_next = rowok ? a.pi[myrow * a.K + k + 1] : 0.0f;
-            __syncthreads();
-            // B operands four k-steps at a time: one ds_read_b128 per column tile (rows
-            // ct*32 + r, LD = D + 4: each 16-lane group of the read covers the 64 banks once),
-            // fetched one group ahead of the MFMAs that consume them.  (The scalar reads the
-            // compiler scheduled just before each MFMA group left the pipe idle on LDS latency:
-            // 13.18 -> 12.62 ms per C4 pass.)
-            float4 bq[CT], bn[CT];
-            float4 mq, mn;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-                bq[ct] = *reinterpret_cast<const float4 *>(Ms + (ct * 32 + r) * LD + S * h);
-            mq = *reinterpret_cast<const float4 *>(mus + S * h);
-#pragma unroll
-            for (int g = 0; g < S / 4; ++g) {
-                if (g + 1 < S / 4) {
-#pragma unroll
-                    for (int ct = 0; ct < CT; ++ct)
-                        bn[ct] = *reinterpret_cast<const float4 *>(Ms + (ct * 32 + r) * LD +
-                                                                    4 * (g + 1) + S * h);
-                    mn = *reinterpret_cast<const float4 *>(mus + 4 * (g + 1) + S * h);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float av = p * (xa[4 * g + i] - mq[i]);
-#pragma unroll
-                    for (int ct = 0; ct < CT; ++ct)
-                        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[ct][i], acc[ct], 0,
-                                                                       0, 0);
-                }
-                if (g + 1 < S / 4) {
-#pragma unroll
-                    for (int ct = 0; ct < CT; ++ct) bq[ct] = bn[ct];
-                    mq = mn;
-                }
-            }
-        }
-        // epilogue: x -= lr * clip(coef * G, -5, 5), through a [128][LD] LDS row tile
-        __syncthreads();
-        float *X = Ms + wid * 32 * LD;  // this wavefront's 32 rows
-#pragma unroll
-        for (int q = 0; q < S; ++q) X[r * LD + q + S * h] = xa[q];
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's rows are in LDS
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-                float *px = X + row * LD + ct * 32 + r;
-                float g = acc[ct][e] * a.coef;
-                g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);
-                *px = *px - g * a.lr;
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < S; ++q) xa[q] = X[r * LD + q + S * h];
-    }
-    if (rowok) {
-#pragma unroll
-        for (int q = 0; q < S; ++q) a.x[myrow * D + q + S * h] = xa[q];
-    }
-}
+// K*d whose A operand is generated on the fly (exact fp32 fmas on the matrix cores).  A workgroup
+// owns 128 rows; the `iters` loop runs in-kernel on the register-resident rows and x is written
+// back once.
 
 // ---- community gradient with asynchronous staging (d in {64, 128}) ----------------------------
 //
-// Same contraction and operand roles as k_community_mfma, restructured so the staging of M_{k+1}
+// The 32x32 fallback (community_async = 1; the default is k_community16 below):
+// v_mfma_f32_32x32x2_f32 (64 cycles), lane (r, h) supplies A[row r][j] and B[j][col r] =
+// M_k[c0 + r][j], 4 wavefronts x 32 rows, CT = d/32 accumulator tiles each; the staging of M_{k+1}
 // overlaps the MFMAs of M_k (the E-step recipe):
 //  * k-step q, half-wave h uses element j(q, h) = 8 (q/4) + 4 h + q%4: four consecutive k-steps of
 //    a lane read one 16-B group g = 2 (q/4) + h of row c = ct*32 + r of M_k (one ds_read_b128).
@@ -843,194 +740,7 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
     }
 }
 
-// Double-buffered E-step: one 8-wavefront workgroup per CU (256 rows, 32 per wavefront, 2
-// wavefronts per SIMD) holds TWO full padded images of P_k^T (2 x 67.6 KB at d = 128) with their
-// mu_k P_k and params.  While component k's MFMAs read buffer k & 1, P_{k+1}^T is copied
-// global -> LDS into the other buffer (global_load_lds_dwordx4, all 8 wavefronts, no VGPRs): one
-// barrier per component instead of two, and no phase of the triangular skip is short of MFMAs to
-// hide its copy behind (k_gmm_resp_mfma's 112 / 48 split).  Same arithmetic, the
-// same MFMA order per column tile and the same epilogue as k_gmm_resp_mfma: bit-identical output.
-template <int D>
-struct RespDbShape {
-    static constexpr int LD = D + 4;                 // padded image row (conflict-free b128 reads)
-    static constexpr int IMG = D * LD;               // floats per image
-    static constexpr int MP = IMG;                   // mu_k P_k (256 reserved)
-    static constexpr int PAR = IMG + 256;            // lower flag, log_norm (64 reserved)
-    static constexpr int BUF = IMG + 256 + 64;       // floats per buffer
-    static constexpr int LDS = 2 * BUF;              // floats
-    static constexpr int WAVES = 8;
-    static_assert(IMG % 256 == 0, "an image is a whole number of 1 KiB copies");
-};
-
-// VAR: the calling kernel's variant.  One instantiation per kernel: the host pass of hipcc
-// rejects a second host-side use of a device template holding global_load_lds.
-template <int D, int VAR>
-__device__ __forceinline__ void resp_db_stage(const RespArgs &a, int k, float *buf, int wid,
-                                              int lane) {
-    using RS = RespDbShape<D>;
-    constexpr int PIECES = RS::IMG / 256;
-    const float *Ptk = a.prec_t + (int64_t)k * D * D;
-#pragma unroll
-    for (int j = 0; j < (PIECES + RS::WAVES - 1) / RS::WAVES; ++j) {
-        const int i = wid + RS::WAVES * j;
-        if (i >= PIECES) break;  // wavefront-uniform
-        const int o = i * 256 + lane * 4;
-        const int c = o / RS::LD, s = o % RS::LD;
-        const int sc = s < D ? s : D - 4;  // padding lanes re-read a valid address
-        __builtin_amdgcn_global_load_lds(Ptk + c * D + sc, buf + i * 256, 16, 0, 0);
-    }
-    if (wid == RS::WAVES - 1) {
-        const int src = lane * 4 < D ? lane * 4 : D - 4;
-        __builtin_amdgcn_global_load_lds(a.mu_prec + (int64_t)k * D + src, buf + RS::MP, 16, 0, 0);
-    } else if (wid == RS::WAVES - 2) {
-        const float *p = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
-                                   : a.log_norm + k;
-        __builtin_amdgcn_global_load_lds(p, buf + RS::PAR, 4, 0, 0);
-    }
-}
-
-// One component's epilogue for a wavefront's 32 x D tile in acc (acc[ct][e] = y - mu_k P_k when
-// FOLD, else y, with mpv[ct] = (mu_k P_k)[ct * 32 + r] subtracted here): the sum of squares over the
-// row, the reduce-scatter over the 32 columns of a half-wave (as k_gmm_resp_mfma), the
-// log-probability store and the online log-sum-exp update.
-template <int D, bool FOLD>
-__device__ __forceinline__ void resp_db_epilogue(
-    const __attribute__((ext_vector_type(16))) float (&acc)[D / 32], const float (&mpv)[D / 32],
-    float lnk, int k, int r, int64_t my_row, const RespArgs &a, float &run_max, float &run_sum) {
-    constexpr int CT = D / 32;
-    float sq[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        sq[e] = 0.0f;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-            const float y = FOLD ? acc[ct][e] : acc[ct][e] - mpv[ct];
-            sq[e] = __builtin_fmaf(y, y, sq[e]);
-        }
-    }
-    const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
-    auto scatter_stage = [](float *v, int n, int keep_hi, auto partner) {
-#pragma unroll
-        for (int i = 0; i < n; ++i) {
-            const float keep = keep_hi ? v[i + n] : v[i];
-            const float send = keep_hi ? v[i] : v[i + n];
-            v[i] = keep + partner(send);
-        }
-    };
-    auto dpp = [](float x, auto ctrl) {
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
-                                                          decltype(ctrl)::value, 0xF, 0xF,
-                                                          false));
-    };
-    scatter_stage(sq, 8, b3, [&](float x) { return dpp(x, std::integral_constant<int, 0x140>{}); });
-    scatter_stage(sq, 4, b2, [&](float x) { return dpp(x, std::integral_constant<int, 0x141>{}); });
-    scatter_stage(sq, 2, b0, [&](float x) { return dpp(x, std::integral_constant<int, 0xB1>{}); });
-    scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
-    const float tot = reduce_stage<4>(sq[0]);  // + the other 16 columns (lane r ^ 16)
-    const float lp = lnk - 0.5f * tot;
-    if (r < 16 && my_row < a.V) a.resp[my_row * a.K + k] = lp;
-    if (lp > run_max) {  // online log-sum-exp of the row's components so far
-        run_sum = run_sum * expf(run_max - lp) + 1.0f;
-        run_max = lp;
-    } else {
-        run_sum += expf(lp - run_max);
-    }
-}
-
-// VAR 1: plain; VAR 2: STAG; VAR 3: STAG + FOLD.
-// STAG: waves 4-7 (the second wave of each SIMD) run each component's epilogue one component
-// late -- at the head of the next component, before its MFMAs -- so on every SIMD one wave's VALU
-// epilogue sits beside its partner's MFMAs instead of both waves reaching it together
-// (MI355X_MICROARCH.md, two waves per SIMD, item 9).  The late waves keep the tile's acc across
-// the barrier and (mu_k P_k, log_norm_k) in registers, since that LDS buffer is re-staged.
-// Outputs are bit-identical to STAG = false.
-// FOLD: the accumulators start at -(mu_k P_k) instead of 0, so the MFMA chain itself forms
-// y - mu_k P_k (64 fewer VALU per component and wavefront; a different fp32 rounding than
-// k_gmm_resp_mfma's, checked against float64).
-template <int D, int VAR>
-__global__ void __launch_bounds__(512, 1) k_gmm_resp_db(RespArgs a) {
-    constexpr bool STAG = VAR >= 2, FOLD = VAR >= 3;
-    using RS = RespDbShape<D>;
-    constexpr int CT = D / 32;
-    constexpr int G = D / 8;
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int tid = threadIdx.x;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int r = lane & 31, h = lane >> 5;
-    const bool late = STAG && wid >= 4;
-    const int64_t blk0 = (int64_t)blockIdx.x * (32 * RS::WAVES);
-    const int64_t myrow = blk0 + wid * 32 + r;
-    const bool rowok = myrow < a.V;
-    f32x4 xa[G];  // xa[g][i] = x[row][8 g + 4 h + i]
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        xa[g] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (rowok) xa[g] = *reinterpret_cast<const f32x4 *>(a.x + myrow * D + 8 * g + 4 * h);
-    }
-    resp_db_stage<D, VAR>(a, 0, sm, wid, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int my_e = 8 * ((r >> 3) & 1) + 4 * ((r >> 2) & 1) + 2 * (r & 1) + ((r >> 1) & 1);
-    const int64_t my_row = blk0 + wid * 32 + (my_e & 3) + 8 * (my_e >> 2) + 4 * h;
-    float run_max = -INFINITY, run_sum = 0.0f;
-    f32x16 acc[CT];
-    float mpv[CT];
-    float lnk_prev = 0.0f;
-    for (int k = 0; k < a.K; ++k) {
-        const float *buf = sm + (k & 1) * RS::BUF;
-        if (k + 1 < a.K) resp_db_stage<D, VAR>(a, k + 1, sm + ((k + 1) & 1) * RS::BUF, wid, lane);
-        const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(buf[RS::PAR])) != 0;
-        const float lnk = buf[RS::PAR + 1];
-        if (late && k > 0)
-            resp_db_epilogue<D, FOLD>(acc, mpv, lnk_prev, k - 1, r, my_row, a, run_max, run_sum);
-        const float *mps = buf + RS::MP;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) mpv[ct] = mps[ct * 32 + r];
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[ct][e] = FOLD ? -mpv[ct] : 0.0f;
-        {
-            auto fetch = [&](int g, f32x4 (&bv)[CT]) {
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
-                    bv[ct] = *reinterpret_cast<const f32x4 *>(buf + (ct * 32 + r) * RS::LD +
-                                                              8 * g + 4 * h);
-            };
-            f32x4 bv[2][CT];
-            fetch(0, bv[0]);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const int cur = g & 1;
-                if (g + 1 < G) fetch(g + 1, bv[cur ^ 1]);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int ct = 0; ct < CT; ++ct) {
-                        if (g >= 4 * (ct + 1) && !full) continue;
-                        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[g][i], bv[cur][ct][i],
-                                                                       acc[ct], 0, 0, 0);
-                    }
-            }
-        }
-        if (!late) resp_db_epilogue<D, FOLD>(acc, mpv, lnk, k, r, my_row, a, run_max, run_sum);
-        lnk_prev = lnk;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // buffer k & 1 free; P_{k+1} in the other buffer
-    }
-    if (late)
-        resp_db_epilogue<D, FOLD>(acc, mpv, lnk_prev, a.K - 1, r, my_row, a, run_max, run_sum);
-    if (r < 16 && my_row < a.V) {
-        float *lp = a.resp + my_row * a.K;
-        const float lse = run_max + logf(run_sum);
-        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
-        if (a.lse) a.lse[my_row] = lse;
-    }
-}
-
-// ---- E-step on v_mfma_f32_16x16x4_f32 (k_gmm_resp16) -------------------------------------------
+// ---- E-step on v_mfma_f32_16x16x4_f32: the FULL body (k_gmm_resp16_full) ------------------
 //
 // Y^T = P_k^T X^T per 16 x 16 tile: A = P_k^T (lane: column c = ct*16 + lane%16, features
 // 16q + 4 (lane/16) + t), B = X^T (lane: row = rt*16 + lane%16, the same features), so the four
@@ -1265,15 +975,6 @@ __device__ __forceinline__ void r16_body(const RespArgs &a, float *sm, int64_t b
     }
 }
 
-template <int D>
-__global__ void __launch_bounds__(256, 2) k_gmm_resp16(RespArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0)
-        r16_body<D, true>(a, sm, blockIdx.x);
-    else
-        r16_body<D, false>(a, sm, blockIdx.x);
-}
-
 // ---- k_gmm_resp16 on packed upper factors: one barrier per component ---------------------------
 //
 // When every factor of the launch is upper-triangular (sklearn's precisions_cholesky_), only the
@@ -1315,24 +1016,23 @@ __global__ void __launch_bounds__(256) k_pack_upper16(const float *__restrict__ 
     }
 }
 
-// Shape of a k_gmm_resp16t variant: VT & 8 = one 16-row tile per wavefront and 8 wavefronts per
-// 128-row workgroup (91-95 VGPRs: 4 waves per SIMD instead of 2 -- the LDS holds two workgroups
-// per CU either way -- at twice the A-operand reads per MFMA); else two row tiles per wavefront
-// and 4 wavefronts (216 VGPRs).
-template <int VT>
+// One 16-row tile per wavefront, 8 wavefronts per 128-row workgroup (91-95 VGPRs: 4 waves per
+// SIMD -- the LDS holds two workgroups per CU either way); two row tiles per wavefront and 4
+// wavefronts (216 VGPRs, 2 waves per SIMD) were bit-identical and 1.5% slower (7.10 vs 7.00 ms).
 struct R16tShape {
-    static constexpr int RT = (VT & 8) ? 1 : 2;  // 16-row tiles per wavefront
-    static constexpr int NW = 8 / RT;            // wavefronts per workgroup
-    static constexpr int ROWS = 16 * RT * NW;    // rows per workgroup (128)
+    static constexpr int NW = 8;                 // wavefronts per workgroup
+    static constexpr int ROWS = 16 * NW;         // rows per workgroup (128)
     static constexpr int THREADS = 64 * NW;
-    static constexpr int WPE = 2 * (3 - RT);     // waves per SIMD the registers must allow: 4 / 2
+    static constexpr int WPE = 4;                // waves per SIMD the registers must allow
 };
 
-// C: the calling kernel (one instantiation each: see r16_stage_mp); NW wavefronts share the copy
-template <int D, int C, int NW>
+// component k's packed blocks, mu_k P_k, lower flag and log_norm into `buf` (NW wavefronts share
+// the 1 KiB copies)
+template <int D>
 __device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf, int wid,
                                            int lane) {
     using T = Resp16T<D>;
+    constexpr int NW = R16tShape::NW;
     const float *src = a.prec_t + (int64_t)k * T::TRI;  // the packed blocks in this body
 #pragma unroll
     for (int j = 0; j < (T::PIECES + NW - 1) / NW; ++j) {
@@ -1366,148 +1066,61 @@ struct TriBlocks {
     }
 };
 
-// All 36 (d = 128) upper blocks of one component on the wavefront's RT row tiles, in row-major
-// order (q, ct >= q); A operands read two blocks ahead through a 3-slot ring.  `after_first` runs
-// once the first A operands are requested (VT & 4: the next component's staging issued behind
-// them).  VT & 1: blocks taken in pairs, the accumulation chains of a pair interleaved.
-template <int D, int VT, typename F>
+// All 36 (d = 128) upper blocks of one component on the wavefront's row tile, in row-major order
+// (q, ct >= q); A operands read two blocks ahead through a 3-slot ring.  (Measured and not kept:
+// blocks in pairs with interleaved accumulation chains +0.5%; the next component's staging issued
+// behind the first A reads 0; a packed-fp32 epilogue 0; the accumulators started at -mu_k P_k and
+// the log-sum-exp after the loop: no gain -- profiles/r04_ab_estep16.txt.)
+template <int D>
 __device__ __forceinline__ void r16t_blocks(
-    const __attribute__((ext_vector_type(4))) float (&xb)[R16tShape<VT>::RT][D / 16],
-    const float *buf, int abase,
-    __attribute__((ext_vector_type(4))) float (&acc)[R16tShape<VT>::RT][D / 16],
-    F &&after_first) {
+    const __attribute__((ext_vector_type(4))) float (&xb)[D / 16], const float *buf, int abase,
+    __attribute__((ext_vector_type(4))) float (&acc)[D / 16]) {
     using T = Resp16T<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int NQ = T::NQ, RT = R16tShape<VT>::RT;
+    constexpr int NQ = T::NQ;
     constexpr int NB = NQ * (NQ + 1) / 2;
     constexpr TriBlocks<NQ> TB{};
     auto fetch = [&](int n) {
         return *reinterpret_cast<const f32x4 *>(buf + T::off(TB.q[n]) + (TB.ct[n] - TB.q[n]) * 256 +
                                                 abase);
     };
-    if constexpr ((VT & 1) == 0) {
-        f32x4 av[3];
-        av[0] = fetch(0);
-        av[1] = fetch(1);
-        after_first();
+    f32x4 av[3];
+    av[0] = fetch(0);
+    av[1] = fetch(1);
 #pragma unroll
-        for (int n = 0; n < NB; ++n) {
-            if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
-            const int q = TB.q[n], ct = TB.ct[n];
+    for (int n = 0; n < NB; ++n) {
+        if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
+        const int q = TB.q[n], ct = TB.ct[n];
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[rt][q][t],
-                                                                       acc[rt][ct], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    } else {
-        static_assert(NB % 2 == 0, "pairs of blocks");
-        f32x4 av[4];  // two pairs: the current one and the next
-        av[0] = fetch(0);
-        av[1] = fetch(1);
-        after_first();
-#pragma unroll
-        for (int n = 0; n < NB; n += 2) {
-            if (n + 2 < NB) {
-                av[(n + 2) % 4] = fetch(n + 2);
-                av[(n + 3) % 4] = fetch(n + 3);
-            }
-            const int q0 = TB.q[n], c0 = TB.ct[n], q1 = TB.q[n + 1], c1 = TB.ct[n + 1];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-                    acc[rt][c0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 4][t], xb[rt][q0][t],
-                                                                       acc[rt][c0], 0, 0, 0);
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-                    acc[rt][c1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        av[(n + 1) % 4][t], xb[rt][q1][t], acc[rt][c1], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        for (int t = 0; t < 4; ++t)
+            acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[q][t], acc[ct], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-// log N(x_row; mu_k, P_k) of the lane's row (row tile kg & 1 when RT = 2) for the component in
-// `buf`.  VT & 2: the epilogue on packed fp32 (v_pk_fma: even and odd columns summed apart, then
-// added -- its own rounding).
-template <int D, int VT, typename F>
-__device__ __forceinline__ float r16t_lp(
-    const __attribute__((ext_vector_type(4))) float (&xb)[R16tShape<VT>::RT][D / 16],
-    const float *buf, int abase, int kg, F &&after_first) {
+// log N(x_row; mu_k, P_k) of the lane's row for the component in `buf`
+template <int D>
+__device__ __forceinline__ float r16t_lp(const __attribute__((ext_vector_type(4))) float (&xb)[D / 16],
+                                         const float *buf, int abase, int kg) {
     using T = Resp16T<D>;
-    constexpr int NQ = T::NQ, RT = R16tShape<VT>::RT;
+    constexpr int NQ = T::NQ;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    using f32x2 = __attribute__((ext_vector_type(2))) float;
     const float lnk = buf[T::PAR + 1];
-    f32x4 acc[RT][NQ];
-    if constexpr ((VT & 32) != 0) {  // accumulators start at -mu_k P_k (own rounding)
+    f32x4 acc[NQ];
 #pragma unroll
-        for (int ct = 0; ct < NQ; ++ct) {
-            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
+    for (int ct = 0; ct < NQ; ++ct) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    r16t_blocks<D>(xb, buf, abase, acc);
+    float sq = 0.0f;
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) acc[rt][ct] = -mp;
+    for (int ct = 0; ct < NQ; ++ct) {
+        const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float y = acc[ct][e] - mp[e];
+            sq = __builtin_fmaf(y, y, sq);
         }
-    } else {
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int ct = 0; ct < NQ; ++ct) acc[rt][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    r16t_blocks<D, VT>(xb, buf, abase, acc, after_first);
-    float sq[RT];
-    if constexpr ((VT & 32) != 0) {
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) sq[rt] = 0.0f;
-#pragma unroll
-        for (int ct = 0; ct < NQ; ++ct)
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sq[rt] = __builtin_fmaf(acc[rt][ct][e], acc[rt][ct][e], sq[rt]);
-    } else if constexpr ((VT & 2) == 0) {
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) sq[rt] = 0.0f;
-#pragma unroll
-        for (int ct = 0; ct < NQ; ++ct) {
-            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float y = acc[rt][ct][e] - mp[e];
-                    sq[rt] = __builtin_fmaf(y, y, sq[rt]);
-                }
-        }
-    } else {
-        f32x2 s2[RT];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) s2[rt] = f32x2{0.0f, 0.0f};
-#pragma unroll
-        for (int ct = 0; ct < NQ; ++ct) {
-            const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const f32x2 y = f32x2{acc[rt][ct][2 * h], acc[rt][ct][2 * h + 1]} -
-                                    f32x2{mp[2 * h], mp[2 * h + 1]};
-                    s2[rt] = __builtin_elementwise_fma(y, y, s2[rt]);
-                }
-        }
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) sq[rt] = s2[rt][0] + s2[rt][1];
-    }
-    const float tot0 = reduce_stage<5>(reduce_stage<4>(sq[0]));
-    if constexpr (RT == 1) {
-        return lnk - 0.5f * tot0;
-    } else {
-        const float tot1 = reduce_stage<5>(reduce_stage<4>(sq[1]));
-        return lnk - 0.5f * ((kg & 1) ? tot1 : tot0);
-    }
+    return lnk - 0.5f * reduce_stage<5>(reduce_stage<4>(sq));
 }
 
 // online log-sum-exp step
@@ -1520,82 +1133,56 @@ __device__ __forceinline__ void lse_push(float lp, float &run_max, float &run_su
     }
 }
 
-template <int D, int VT>
-__device__ __forceinline__ void r16t_body(const RespArgs &a, float *sm) {
+// The default E-step when every factor of the launch is upper-triangular (flags[K] == 0); a
+// launch holding a lower or dense factor returns at once and k_gmm_resp16_full (launched after it)
+// runs every block.  prec_t points to the packed blocks, prec_full to P^T.
+template <int D>
+__global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp16t(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0) return;
     using T = Resp16T<D>;
-    using S = R16tShape<VT>;
-    constexpr int NQ = T::NQ, RT = S::RT;
+    constexpr int NQ = T::NQ;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int j16 = lane & 15, kg = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * S::ROWS + wid * 16 * RT;
-    f32x4 xb[RT][NQ];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-        const int64_t row = row0 + 16 * rt + j16;
+    const int64_t row0 = (int64_t)blockIdx.x * R16tShape::ROWS + wid * 16;
+    f32x4 xb[NQ];  // xb[q][t] = x[row0 + j16][16 q + 4 kg + t]
+    {
+        const int64_t row = row0 + j16;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            xb[rt][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            if (row < a.V) xb[rt][q] = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg);
+            xb[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (row < a.V) xb[q] = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg);
         }
     }
-    r16t_stage<D, VT, S::NW>(a, 0, sm, wid, lane);
+    r16t_stage<D>(a, 0, sm, wid, lane);
     // the lane's A operands of block (q, ct): row ct*16 + j16 of quad q's row block
     const int abase = j16 * 16 + 4 * (kg ^ ((j16 >> 1) & 2));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // RT = 2: lanes 0-15 own row tile 0, lanes 16-31 row tile 1; RT = 1: lanes 0-15
-    const int64_t my_row = row0 + (RT == 2 ? 16 * (kg & 1) : 0) + j16;
-    const bool owner = kg < RT && my_row < a.V;
+    const int64_t my_row = row0 + j16;  // lanes 0-15 own the tile's rows
+    const bool owner = kg == 0 && my_row < a.V;
     float run_max = -INFINITY, run_sum = 0.0f;
     for (int k = 0; k < a.K; ++k) {
         const float *buf = sm + (k & 1) * T::BUF;
-        auto stage_next = [&] {
-            if (k + 1 < a.K)
-                r16t_stage<D, VT, S::NW>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
-        };
-        if constexpr ((VT & 4) == 0) stage_next();
-        const float lp = r16t_lp<D, VT>(xb, buf, abase, kg, [&] {
-            if constexpr ((VT & 4) != 0) stage_next();
-        });
+        if (k + 1 < a.K) r16t_stage<D>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
+        const float lp = r16t_lp<D>(xb, buf, abase, kg);
         if (owner) a.resp[my_row * a.K + k] = lp;
-        if constexpr ((VT & 16) == 0) lse_push(lp, run_max, run_sum);
+        lse_push(lp, run_max, run_sum);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
     }
     if (owner) {
         float *lp = a.resp + my_row * a.K;
-        if constexpr ((VT & 16) != 0) {  // VT & 16: the log-sum-exp after the loop (max first)
-            for (int k = 0; k < a.K; ++k) run_max = fmaxf(run_max, lp[k]);
-            for (int k = 0; k < a.K; ++k) run_sum += expf(lp[k] - run_max);
-        }
         const float lse = run_max + logf(run_sum);
         for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
         if (a.lse) a.lse[my_row] = lse;
     }
 }
 
-// gmm_resp16 = 2: the packed, one-barrier form when every factor is upper-triangular (flags[K] ==
-// 0), else k_gmm_resp16's FULL body (on the first four wavefronts; with 8, the others run it
-// with no rows so that every barrier is met); prec_t points to the packed blocks, prec_full to P^T.
-template <int D, int VT>
-__global__ void __launch_bounds__(R16tShape<VT>::THREADS, R16tShape<VT>::WPE)
-    k_gmm_resp16t(RespArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0) {
-        if constexpr (R16tShape<VT>::RT == 2) {
-            RespArgs b = a;
-            b.prec_t = a.prec_full;
-            r16_body<D, true>(b, sm, blockIdx.x);
-        }
-    } else {
-        r16t_body<D, VT>(a, sm);
-    }
-}
-
-// The FULL body for the one-row-tile variants (whose registers cannot hold it), launched after
-// them: a no-op unless the launch holds a lower or dense factor (flags[K]); row blocks grid-stride.
+// The FULL body (k_gmm_resp16t's registers cannot hold it), launched after it: a no-op unless the
+// launch holds a lower or dense factor (flags[K]); row blocks grid-stride.
 template <int D>
 __global__ void __launch_bounds__(256, 2) k_gmm_resp16_full(RespArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1630,15 +1217,12 @@ struct CovArgs {
 };
 
 // Symmetric output: only the CT (CT + 1) / 2 tiles with rt <= ct are accumulated (10 of 16 at
-// d = 128, 3 of 4 at d = 64), TPW per wavefront over kCovWaves<D> wavefronts, and each off-diagonal
-// tile is also stored transposed -- S_k comes out exactly symmetric.
+// d = 128, 3 of 4 at d = 64), and each off-diagonal tile is also stored transposed -- S_k comes out
+// exactly symmetric.
 template <int D>
 struct CovShape {
     static constexpr int CT = D / 32;
     static constexpr int NT = CT * (CT + 1) / 2;
-    static constexpr int TPW = D == 128 ? 2 : 1;
-    static constexpr int WAVES = NT / TPW;  // 5 (d = 128), 3 (d = 64)
-    static_assert(NT % TPW == 0, "tiles must split evenly over the wavefronts");
     // k_gmm_cov_async: CPW components per workgroup, 4 MFMA wavefronts (one per SIMD) with ATPW
     // tiles each -- the CPW * NT tiles split evenly (2 x 10 = 4 x 5 at d = 128, 4 x 3 = 4 x 3 at
     // 64) -- plus 4 staging wavefronts
@@ -1657,72 +1241,6 @@ __device__ __forceinline__ void upper_tile(int t, int CT, int &rt, int &ct) {
         ++rt;
     }
     ct = rt + t;
-}
-
-template <int D>
-__global__ void __launch_bounds__(64 * CovShape<D>::WAVES) k_gmm_cov_mfma(CovArgs a) {
-    constexpr int CT = CovShape<D>::CT;
-    constexpr int TPW = CovShape<D>::TPW;
-    constexpr int NTH = 64 * CovShape<D>::WAVES;
-    constexpr int LD = D + 4;
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
-    __shared__ __attribute__((aligned(16))) float xs[kCovRB * LD];
-    __shared__ float ws[kCovRB];
-    __shared__ float mus[D];
-    const int k = blockIdx.x;
-    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
-    int64_t c1 = c0 + a.rows_per_chunk;
-    if (c1 > a.V) c1 = a.V;
-    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    const int r = lane & 31, h = lane >> 5;
-    int rts[TPW], cts[TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) upper_tile(wid * TPW + t, CT, rts[t], cts[t]);
-    if (tid < D) mus[tid] = a.means[k * D + tid];
-    f32x16 acc[TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
-    for (int64_t b = c0; b < c1; b += kCovRB) {
-        __syncthreads();
-        for (int o = tid; o < kCovRB * D / 4; o += NTH) {
-            const int s = (o * 4) / D, c = (o * 4) % D;
-            const int64_t row = b + s;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row < c1) v = reinterpret_cast<const float4 *>(a.x + row * D)[c / 4];
-            float *dst = xs + s * LD + c;
-            dst[0] = v.x - mus[c];
-            dst[1] = v.y - mus[c + 1];
-            dst[2] = v.z - mus[c + 2];
-            dst[3] = v.w - mus[c + 3];
-        }
-        if (tid < kCovRB) ws[tid] = b + tid < c1 ? a.resp[(b + tid) * a.K + k] : 0.0f;
-        __syncthreads();
-#pragma unroll 4
-        for (int s0 = 0; s0 < kCovRB; s0 += 2) {
-            const float *row = xs + (s0 + h) * LD;
-            const float w = ws[s0 + h];
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) {
-                const float av = w * row[rts[t] * 32 + r];
-                const float bv = row[cts[t] * 32 + r];
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
-            }
-        }
-    }
-    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * D * D;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        const int rt = rts[t], ct = cts[t];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int i = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int j = ct * 32 + r;
-            out[(int64_t)i * D + j] = acc[t][e];
-            if (rt != ct) out[(int64_t)j * D + i] = acc[t][e];
-        }
-    }
 }
 
 // The upper tiles T0 .. T0 + ATPW - 1 of one component (one MFMA wavefront's share), with the
@@ -1790,10 +1308,10 @@ struct CovTiles {
     }
 };
 
-// NBUF image buffers: 3 -> one workgroup per CU, the MFMA wavefronts read a block's first
-// operands before the barrier that starts it; 2 -> two workgroups per CU (<= 128 registers per
-// wavefront), the other workgroup's MFMA wavefront covers each one's barrier.
-template <int D, int NBUF_>
+// Two image buffers, two workgroups per CU (<= 128 registers per wavefront): the other
+// workgroup's MFMA wavefront covers each one's barrier.  (Three buffers and one workgroup per CU,
+// reading the next block's first operands before its barrier: 8.7 vs 7.9 ms at C4.)
+template <int D>
 struct CovAsync {
     static constexpr int RB = 32;                         // samples per block
     static constexpr int LDT = RB + 4;                    // padded row of a transposed image
@@ -1801,20 +1319,18 @@ struct CovAsync {
     static constexpr int CPW = CovShape<D>::CPW;
     static constexpr int WOFF = CPW * IMG;                // weights [CPW][RB] after the images
     static constexpr int BUF = CPW * IMG + CPW * RB;      // floats per buffer
-    static constexpr int NBUF = NBUF_;
-    static constexpr int OPB = NBUF == 3 ? 2 : 1;         // operand register sets
-    static constexpr int WPE = NBUF == 3 ? 2 : 4;         // waves per SIMD the kernel is built for
+    static constexpr int NBUF = 2;
+    static constexpr int WPE = 4;                         // waves per SIMD the kernel is built for
 };
 
-// One MFMA wavefront over all nb blocks.  OPB == 2: operands of group g + 1 (or, NBUF == 3, of
-// the next block's group 0, staged two barriers earlier) are read while group g's MFMAs run.
-template <int D, int T0, int NBUF>
+// One MFMA wavefront over all nb blocks: one operand register set, group g + 1's operands read
+// after group g's MFMAs are issued.
+template <int D, int T0>
 __device__ __forceinline__ void cov_consume(const float *img, int nb, int tk, int lane,
                                             __attribute__((ext_vector_type(16)))
                                             float (&acc)[CovShape<D>::ATPW]) {
     using TS = CovTiles<D, T0>;
-    using CA = CovAsync<D, NBUF>;
-    constexpr int OPB = CA::OPB;
+    using CA = CovAsync<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr int N = TS::N;
     constexpr int NA = TS::template count<true>();
@@ -1830,43 +1346,35 @@ __device__ __forceinline__ void cov_consume(const float *img, int nb, int tk, in
     const int wb = CA::WOFF + tk * CA::RB + 4 * h;
     constexpr typename TS::Table IA = TS::template idx_table<true>();
     constexpr typename TS::Table IB = TS::template idx_table<false>();
-    f32x4 ra[OPB][NA], rb[OPB][NB], rw[OPB];
-    auto fetch = [&](int blk, int g, int slot) {
+    f32x4 ra[NA], rb[NB], rw;
+    auto fetch = [&](int blk, int g) {
         const float *buf = img + (blk % CA::NBUF) * CA::BUF + 8 * g;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) ra[slot][i] = *reinterpret_cast<const f32x4 *>(buf + ab[i]);
+        for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const f32x4 *>(buf + ab[i]);
 #pragma unroll
-        for (int i = 0; i < NB; ++i) rb[slot][i] = *reinterpret_cast<const f32x4 *>(buf + bb[i]);
-        rw[slot] = *reinterpret_cast<const f32x4 *>(buf + wb);
+        for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const f32x4 *>(buf + bb[i]);
+        rw = *reinterpret_cast<const f32x4 *>(buf + wb);
     };
     for (int j = 0; j < nb; ++j) {
-        if (NBUF == 2 || j == 0) {
-            __syncthreads();  // barrier j: block j staged
-            fetch(j, 0, 0);
-        }
+        __syncthreads();  // barrier j: block j staged
+        fetch(j, 0);
 #pragma unroll
         for (int g = 0; g < CA::RB / 8; ++g) {
-            const int cur = OPB == 2 ? (g & 1) : 0;  // RB / 8 is even: group 0 is slot 0
-            if (OPB == 2) {
-                if (g + 1 < CA::RB / 8) fetch(j, g + 1, cur ^ 1);
-                else if (NBUF == 3 && j + 1 < nb) fetch(j + 1, 0, cur ^ 1);
-            }
-            f32x4 wa[NA];  // A = r * (x - mu), the synchronous form's product
+            f32x4 wa[NA];  // A = r * (x - mu): every MFMA operand an exact fp32 product
 #pragma unroll
-            for (int i = 0; i < NA; ++i) wa[i] = rw[cur] * ra[cur][i];
+            for (int i = 0; i < NA; ++i) wa[i] = rw * ra[i];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int t = 0; t < N; ++t)
                     acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                        wa[IA.v[t]][q], rb[cur][IB.v[t]][q], acc[t], 0, 0, 0);
-            if (OPB == 1 && g + 1 < CA::RB / 8) fetch(j, g + 1, 0);
+                        wa[IA.v[t]][q], rb[IB.v[t]][q], acc[t], 0, 0, 0);
+            if (g + 1 < CA::RB / 8) fetch(j, g + 1);
         }
-        if (NBUF == 3 && j + 1 < nb) __syncthreads();  // barrier j + 1
     }
 }
 
-// Default form ("gmm_cov_async" = 0 selects the synchronous k_gmm_cov_mfma).  What limited the
+// The 32x32 fallback (gmm_cov_async = 1; the default is k_gmm_cov16 below).  What limited the
 // earlier forms (SQ counters at C4, profiles/r01h_c4_pmc_sq.txt, profiles/r02_c4_scatter_ab.txt):
 // VALU work per MFMA (every operand centred and weighted at read time: 8.6 VALU per MFMA), SIMD
 // imbalance (5-wavefront workgroups put two tile sets on one SIMD of four), MFMA wavefronts
@@ -1879,19 +1387,17 @@ __device__ __forceinline__ void cov_consume(const float *img, int nb, int tk, in
 //    (rows padded to 36 floats) and its weights r_sk stored beside it.  The MFMA wavefronts form
 //    A = r_sk * B[k][c][s] in registers (the synchronous form's fp32 subtraction and product:
 //    every MFMA operand is bit-identical), 4 VALU per distinct A row per 20 MFMAs;
-//  * image buffers: NBUF = 2 (default) -> block j + 1 is staged while block j is multiplied,
-//    74 KB, two workgroups per CU whose MFMA wavefronts cover each other's barriers; NBUF = 3 ->
-//    111 KB, one workgroup per CU that reads the next block's first operands before its barrier.
-//    One barrier per block either way;
+//  * two image buffers: block j + 1 is staged while block j is multiplied, 74 KB, two workgroups
+//    per CU whose MFMA wavefronts cover each other's barriers; one barrier per block;
 //  * the k-steps pair samples s(q, h) = 8 (q/4) + 4 h + q%4, so the four consecutive k-steps of
 //    a lane read one 16-byte group of a row: one ds_read_b128 per distinct operand row per 4
 //    MFMAs (6 or 5 rows for a wavefront's 5 tiles at d = 128), and the padding sends the 16
 //    lanes of each b128 phase to 16 distinct 4-bank groups.
-// C4 (V = 1M, K = 50, d = 128): 7.9 ms (NBUF 2) / 8.7 ms (NBUF 3) vs 11.3 ms for round 1's form.
-template <int D, int NBUF>
+// C4 (V = 1M, K = 50, d = 128): 7.9 ms vs 11.3 ms for round 1's synchronous form.
+template <int D>
 __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
-    __attribute__((amdgpu_waves_per_eu(CovAsync<D, NBUF>::WPE))) k_gmm_cov_async(CovArgs a) {
-    using CA = CovAsync<D, NBUF>;
+    __attribute__((amdgpu_waves_per_eu(CovAsync<D>::WPE))) k_gmm_cov_async(CovArgs a) {
+    using CA = CovAsync<D>;
     constexpr int NT = CovShape<D>::NT;
     constexpr int CPW = CA::CPW;
     constexpr int TPW = CovShape<D>::ATPW;
@@ -1920,8 +1426,8 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
         if (nb > 0) {
-            if (t0 == 0) cov_consume<D, 0, NBUF>(img, nb, tk, lane, acc);
-            else cov_consume<D, (NT == TPW ? 0 : TPW), NBUF>(img, nb, tk, lane, acc);
+            if (t0 == 0) cov_consume<D, 0>(img, nb, tk, lane, acc);
+            else cov_consume<D, (NT == TPW ? 0 : TPW)>(img, nb, tk, lane, acc);
         }
         if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
         const int r = lane & 31, h = lane >> 5;
@@ -1982,7 +1488,7 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
         if (wlane) buf[CA::WOFF + wk * RB + SPT * sp + ws] = wr;
     };
     if (nb == 0) return;
-    constexpr int SD = NBUF - 1;  // block j + SD is staged while block j is multiplied
+    constexpr int SD = CA::NBUF - 1;  // block j + SD is staged while block j is multiplied
 #pragma unroll
     for (int u = 0; u < 3; ++u)
         if (u < nb) load(u, xv[u], wl[u]);
@@ -2020,10 +1526,9 @@ __global__ void __launch_bounds__(CovShape<D>::ATHREADS)
 // conflict-free without padding).  A d = 128 component's 36 tiles split 18 / 18 over two
 // wavefronts by tile rows {0, 1, 6, 7} and {2, 3, 4, 5}; a wavefront weights its 4 A rows once
 // per group and streams the B rows column by column (few VGPRs at 4 waves per SIMD).
-// W = 1 (gmm_cov_async = 4): twice the MFMA wavefronts, each with half the tiles (tile rows
-// {p, NT16 - 1 - p}: 9 tiles at d = 128, 5 at 64), so 8 MFMA + 4 staging wavefronts per workgroup
-// and 4 MFMA waves per SIMD instead of 2 (the E-step / community lesson).
-template <int D, int W = 0>
+// (Twice the MFMA wavefronts with half the tiles each -- 4 MFMA waves per SIMD, the E-step /
+// community lesson -- was bit-identical and no faster: 7.45 vs 7.35 ms, profiles/r04_ab_scatter16.txt.)
+template <int D>
 struct Cov16 {
     static constexpr int RB = 32;                 // samples per block
     static constexpr int LDT = RB;                // image row (swizzled, unpadded)
@@ -2033,25 +1538,24 @@ struct Cov16 {
     static constexpr int BUF = CPW * IMG + CPW * RB;
     static constexpr int NBUF = 2;
     static constexpr int NT16 = D / 16;
-    static constexpr int WPC = (D == 128 ? 2 : 1) * (W ? 2 : 1);  // MFMA wavefronts per component
+    static constexpr int WPC = D == 128 ? 2 : 1;                  // MFMA wavefronts per component
     static constexpr int NTW = NT16 * (NT16 + 1) / 2 / WPC;      // tiles per wavefront
-    static constexpr int NR = W ? 2 : 4;                          // A rows per wavefront
+    static constexpr int NR = 4;                                  // A rows per wavefront
     static constexpr int AW = CPW * WPC;                          // MFMA wavefronts
     static constexpr int THREADS = 64 * (AW + 4);                 // + 4 staging wavefronts
 };
 
-// Tiles of MFMA wavefront part p (W = 0: 0 / 1 at d = 128, 0 at d = 64) in issue order
-// (column-major: B row ct once per column), with their A-row slot.
-template <int D, int W = 0>
+// Tiles of MFMA wavefront part p (0 / 1 at d = 128, 0 at d = 64) in issue order (column-major:
+// B row ct once per column), with their A-row slot.
+template <int D>
 struct Cov16Tiles {
-    using C = Cov16<D, W>;
+    using C = Cov16<D>;
     int rows[C::WPC][C::NR];
     int ct[C::WPC][C::NTW], slot[C::WPC][C::NTW];
     constexpr Cov16Tiles() : rows(), ct(), slot() {
         for (int p = 0; p < C::WPC; ++p) {
             for (int i = 0; i < C::NR; ++i)
-                rows[p][i] = W ? (i == 0 ? p : C::NT16 - 1 - p)
-                               : (D == 64 ? i : (p == 0 ? (i < 2 ? i : i + 4) : i + 2));
+                rows[p][i] = D == 64 ? i : (p == 0 ? (i < 2 ? i : i + 4) : i + 2);
             int n = 0;
             for (int c = 0; c < C::NT16; ++c)
                 for (int i = 0; i < C::NR; ++i)
@@ -2069,13 +1573,13 @@ __device__ __forceinline__ int cov16_off(int c, int gran) {  // image offset of 
     return c * Cov16<D>::LDT + 4 * (gran ^ (c & 7));
 }
 
-template <int D, int W, int P>
+template <int D, int P>
 __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, int lane,
                                               __attribute__((ext_vector_type(4)))
-                                              float (&acc)[Cov16<D, W>::NTW]) {
-    using C = Cov16<D, W>;
+                                              float (&acc)[Cov16<D>::NTW]) {
+    using C = Cov16<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr Cov16Tiles<D, W> TT{};
+    constexpr Cov16Tiles<D> TT{};
     const int j16 = lane & 15, kg = lane >> 4;
     for (int j = 0; j < nb; ++j) {
         __syncthreads();  // barrier j: block j staged
@@ -2110,17 +1614,17 @@ __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, 
 }
 
 // the MFMA part of wavefront part P (compile-time tile tables): consume, then store the tiles
-template <int D, int W, int P>
+template <int D, int P>
 __device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, int nb, int tk,
                                            int nk, int k0, int lane) {
-    using C = Cov16<D, W>;
+    using C = Cov16<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     f32x4 acc[C::NTW];
 #pragma unroll
     for (int n = 0; n < C::NTW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (nb > 0) cov16_consume<D, W, P>(img, nb, tk, lane, acc);
+    if (nb > 0) cov16_consume<D, P>(img, nb, tk, lane, acc);
     if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
-    constexpr Cov16Tiles<D, W> TT{};
+    constexpr Cov16Tiles<D> TT{};
     const int j16 = lane & 15, kg = lane >> 4;
     float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
 #pragma unroll
@@ -2136,10 +1640,10 @@ __device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, i
     }
 }
 
-template <int D, int W>
-__global__ void __launch_bounds__((Cov16<D, W>::THREADS))
-    __attribute__((amdgpu_waves_per_eu(W ? 6 : 4))) k_gmm_cov16(CovArgs a) {
-    using C = Cov16<D, W>;
+template <int D>
+__global__ void __launch_bounds__((Cov16<D>::THREADS))
+    __attribute__((amdgpu_waves_per_eu(4))) k_gmm_cov16(CovArgs a) {
+    using C = Cov16<D>;
     constexpr int CPW = C::CPW;
     constexpr int NST = 256;  // staging threads (4 wavefronts)
     constexpr int RB = C::RB;
@@ -2158,11 +1662,9 @@ __global__ void __launch_bounds__((Cov16<D, W>::THREADS))
     if (wid < C::AW) {
         // ---- MFMA wavefronts: component tk, tile part p ----
         const int tk = wid / C::WPC, p = wid % C::WPC;
-        constexpr int P1 = C::WPC > 1 ? 1 : 0, P2 = C::WPC > 2 ? 2 : 0, P3 = C::WPC > 3 ? 3 : 0;
-        if (p == 0) cov16_part<D, W, 0>(a, img, nb, tk, nk, k0, lane);
-        else if (p == 1) cov16_part<D, W, P1>(a, img, nb, tk, nk, k0, lane);
-        else if (p == 2) cov16_part<D, W, P2>(a, img, nb, tk, nk, k0, lane);
-        else cov16_part<D, W, P3>(a, img, nb, tk, nk, k0, lane);
+        constexpr int P1 = C::WPC > 1 ? 1 : 0;
+        if (p == 0) cov16_part<D, 0>(a, img, nb, tk, nk, k0, lane);
+        else cov16_part<D, P1>(a, img, nb, tk, nk, k0, lane);
         return;
     }
     // ---- staging wavefronts (as k_gmm_cov_async): thread owns column sc and samples SPT sp ..
@@ -2172,8 +1674,8 @@ __global__ void __launch_bounds__((Cov16<D, W>::THREADS))
     float mu[CPW];
 #pragma unroll
     for (int kk = 0; kk < CPW; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
-    float xv[W ? 2 : 3][SPT];
-    float wl[W ? 2 : 3];
+    float xv[3][SPT];
+    float wl[3];
     const int wk = lane / SPT, ws = lane % SPT;
     const bool wlane = lane < SPT * CPW;
     auto load = [&](int blk, float (&xr)[SPT], float &wr) {
@@ -2205,46 +1707,24 @@ __global__ void __launch_bounds__((Cov16<D, W>::THREADS))
     };
     if (nb == 0) return;
     constexpr int SD = C::NBUF - 1;  // block j + 1 is staged while block j is multiplied
-    if constexpr (W == 0) {
 #pragma unroll
-        for (int u = 0; u < 3; ++u)
-            if (u < nb) load(u, xv[u], wl[u]);
-        if (0 < nb) {
-            stage(0, xv[0], wl[0]);
-            if (3 < nb) load(3, xv[0], wl[0]);
-        }
-        __syncthreads();  // barrier 0
-        for (int j0 = 0; j0 < nb; j0 += 3) {
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
-                const int j = j0 + u;
-                if (j >= nb) break;
-                if (j + SD < nb) {
-                    stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-                    if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-                }
-                if (j + 1 < nb) __syncthreads();  // barrier j + 1
-            }
-        }
-    } else {
-        // two register sets (the registers 6 waves per SIMD allow): block b lives in set b % 2,
-        // loaded two blocks before it is staged
-        load(0, xv[0], wl[0]);
-        if (1 < nb) load(1, xv[1], wl[1]);
+    for (int u = 0; u < 3; ++u)
+        if (u < nb) load(u, xv[u], wl[u]);
+    if (0 < nb) {
         stage(0, xv[0], wl[0]);
-        if (2 < nb) load(2, xv[0], wl[0]);
-        __syncthreads();  // barrier 0
-        for (int j0 = 0; j0 < nb; j0 += 2) {
+        if (3 < nb) load(3, xv[0], wl[0]);
+    }
+    __syncthreads();  // barrier 0
+    for (int j0 = 0; j0 < nb; j0 += 3) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {  // j = j0 + u: block j + 1 in set (u + 1) % 2
-                const int j = j0 + u;
-                if (j >= nb) break;
-                if (j + 1 < nb) {
-                    stage(j + 1, xv[(u + 1) % 2], wl[(u + 1) % 2]);
-                    if (j + 3 < nb) load(j + 3, xv[(u + 1) % 2], wl[(u + 1) % 2]);
-                }
-                if (j + 1 < nb) __syncthreads();  // barrier j + 1
+        for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
+            const int j = j0 + u;
+            if (j >= nb) break;
+            if (j + SD < nb) {
+                stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
+                if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
             }
+            if (j + 1 < nb) __syncthreads();  // barrier j + 1
         }
     }
 }
@@ -2472,54 +1952,30 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     int rc = ensure_init(&dev);
     if (rc) return rc;
     CommArgs a{x, pi, mu, inv_cov, V, d, K, (float)((double)beta / (double)K), lr, iters};
-    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 &&
-        ((uintptr_t)mu % 16) == 0 && current_opts().community_async == 2) {
-        const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(d == 64 ? Comm16<64>::LDS_FLOATS
-                                                            : Comm16<128>::LDS_FLOATS);
-        static bool attr_16 = false;
-        if (!attr_16) {
-            (void)hipFuncSetAttribute((const void *)k_community16<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_community16<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr_16 = true;
+    const int variant = current_opts().community_async;
+    if (variant != 1 && variant != 2)
+        return set_error(COME_E_INVALID, "community_async must be 1 or 2 (got %d)", variant);
+    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 && ((uintptr_t)mu % 16) == 0) {
+        // 2 (default): k_community16; 1: the 32x32 fallback k_community_async
+        void (*kern)(CommArgs) = variant == 2 ? (d == 64 ? k_community16<64> : k_community16<128>)
+                                              : (d == 64 ? k_community_async<64>
+                                                         : k_community_async<128>);
+        const size_t lds = sizeof(float) *
+                           (size_t)(variant == 2 ? (d == 64 ? Comm16<64>::LDS_FLOATS
+                                                            : Comm16<128>::LDS_FLOATS)
+                                                 : (d == 64 ? CommAsync<64>::LDS_FLOATS
+                                                            : CommAsync<128>::LDS_FLOATS));
+        static bool attr = false;
+        if (!attr) {
+            for (void (*f)(CommArgs) : {k_community16<64>, k_community16<128>,
+                                        k_community_async<64>, k_community_async<128>})
+                (void)hipFuncSetAttribute((const void *)f,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
         }
-        hipLaunchKernelGGL(d == 64 ? k_community16<64> : k_community16<128>, dim3(grid), dim3(512),
+        hipLaunchKernelGGL(kern, dim3((unsigned)((V + 127) / 128)), dim3(variant == 2 ? 512 : 256),
                            lds, (hipStream_t)stream, a);
-        return hip_error(hipGetLastError(), "k_community16 launch");
-    }
-    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 &&
-        ((uintptr_t)mu % 16) == 0 && current_opts().community_async) {
-        const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(d == 64 ? CommAsync<64>::LDS_FLOATS
-                                                            : CommAsync<128>::LDS_FLOATS);
-        void (*kern)(CommArgs) = d == 64 ? k_community_async<64> : k_community_async<128>;
-        static bool attr_a = false;
-        if (!attr_a) {
-            (void)hipFuncSetAttribute((const void *)k_community_async<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_community_async<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr_a = true;
-        }
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
-        return hip_error(hipGetLastError(), "k_community_async launch");
-    }
-    if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0) {
-        const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(128 * (d + 4) + d);
-        void (*kern)(CommArgs) = d == 64 ? k_community_mfma<64> : k_community_mfma<128>;
-        static bool attr_m = false;
-        if (!attr_m) {
-            (void)hipFuncSetAttribute((const void *)k_community_mfma<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_community_mfma<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr_m = true;
-        }
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
-        return hip_error(hipGetLastError(), "k_community_mfma launch");
+        return hip_error(hipGetLastError(), "community MFMA launch");
     }
     if (d > 128) {
         const size_t lds = sizeof(float) * ((size_t)3 * kTRW * d +
@@ -2536,11 +1992,11 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     }
     const size_t lds = sizeof(float) * ((size_t)3 * kTR * d + (size_t)d * d);
     const unsigned grid = (unsigned)((V + kTR - 1) / kTR);
-    static bool attr = false;
-    if (!attr) {
+    static bool attr_v = false;
+    if (!attr_v) {
         (void)hipFuncSetAttribute((const void *)k_community_grad,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
+        attr_v = true;
     }
     hipLaunchKernelGGL(k_community_grad, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, a);
     return hip_error(hipGetLastError(), "k_community_grad launch");
@@ -2586,22 +2042,9 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         if (rc) return rc;
         a.prec_t = pt;
         const int r16 = current_opts().gmm_resp16;
-        // k_gmm_resp16t variants (VT): 0 = two row tiles per wavefront, 2 = + packed epilogue,
-        // 8 = one row tile (the default: 7.00 vs 7.10 ms at C4, bit-identical to 0), 10 = one row
-        // tile + packed epilogue (7.01 ms; profiles/r04_ab_estep16.txt; 10-wavefront workgroups
-        // of VT 8: 8.7 ms).  gmm_resp16 = 2: VT 8; 16 + i: entry i (A/B)
-        // (A/B, late round 3: 24 = 8 with the log-sum-exp after the loop, 40 = 8 with the
-        // accumulators started at -mu_k P_k, 56 = both: gmm_resp16 = 20, 21, 22)
-        static const int kVts[7] = {0, 2, 8, 10, 24, 40, 56};
-        static void (*const k_r16t[7][2])(RespArgs) = {
-            {k_gmm_resp16t<64, 0>, k_gmm_resp16t<128, 0>},
-            {k_gmm_resp16t<64, 2>, k_gmm_resp16t<128, 2>},
-            {k_gmm_resp16t<64, 8>, k_gmm_resp16t<128, 8>},
-            {k_gmm_resp16t<64, 10>, k_gmm_resp16t<128, 10>},
-            {k_gmm_resp16t<64, 24>, k_gmm_resp16t<128, 24>},
-            {k_gmm_resp16t<64, 40>, k_gmm_resp16t<128, 40>},
-            {k_gmm_resp16t<64, 56>, k_gmm_resp16t<128, 56>}};
-        if (r16 == 2 || (r16 >= 16 && r16 < 23)) {
+        if (r16 == 2) {
+            // default: k_gmm_resp16t over the packed non-zero blocks (every factor upper-
+            // triangular), then k_gmm_resp16_full (a no-op unless some factor is lower or dense)
             const int tri = d == 64 ? Resp16T<64>::TRI : Resp16T<128>::TRI;
             float *packed = stream_scratch(dev, stream, kScratchGmmTri, sizeof(float) * (size_t)K * tri);
             if (!packed) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
@@ -2613,74 +2056,31 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
             RespArgs b = a;
             b.prec_full = a.prec_t;
             b.prec_t = packed;
-            const size_t ldst = sizeof(float) * (size_t)std::max(
-                d == 64 ? Resp16T<64>::LDS : Resp16T<128>::LDS,
-                d == 64 ? Resp16Shape<64>::LDS : Resp16Shape<128>::LDS);
+            const size_t ldst = sizeof(float) * (size_t)(d == 64 ? Resp16T<64>::LDS : Resp16T<128>::LDS);
+            const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
+                                                                   : Resp16Shape<128>::LDS);
             static bool attr16t = false;
             if (!attr16t) {
-                for (int v = 0; v < 7; ++v)
-                    for (int dd = 0; dd < 2; ++dd)
-                        (void)hipFuncSetAttribute((const void *)k_r16t[v][dd],
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  160 * 1024);
-                for (void (*f)(RespArgs) : {k_gmm_resp16_full<64>, k_gmm_resp16_full<128>})
+                for (void (*f)(RespArgs) : {k_gmm_resp16t<64>, k_gmm_resp16t<128>,
+                                            k_gmm_resp16_full<64>, k_gmm_resp16_full<128>})
                     (void)hipFuncSetAttribute((const void *)f,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr16t = true;
             }
-            const int vi = r16 >= 16 ? r16 - 16 : 2;
-            const int vt = kVts[vi];
-            hipLaunchKernelGGL(k_r16t[vi][d == 64 ? 0 : 1], dim3((unsigned)((V + 127) / 128)),
-                               dim3((vt & 8) ? 512 : 256), ldst, (hipStream_t)stream, b);
+            hipLaunchKernelGGL(d == 64 ? k_gmm_resp16t<64> : k_gmm_resp16t<128>,
+                               dim3((unsigned)((V + 127) / 128)), dim3(R16tShape::THREADS), ldst,
+                               (hipStream_t)stream, b);
             rc = hip_error(hipGetLastError(), "k_gmm_resp16t launch");
-            if (rc || !(vt & 8)) return rc;
+            if (rc) return rc;
             const int64_t blks = (V + 127) / 128;
-            const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
-                                                                   : Resp16Shape<128>::LDS);
             hipLaunchKernelGGL(d == 64 ? k_gmm_resp16_full<64> : k_gmm_resp16_full<128>,
                                dim3((unsigned)std::min<int64_t>(blks, 2 * (int64_t)num_cus(dev))),
                                dim3(256), lds16, (hipStream_t)stream, b);
             return hip_error(hipGetLastError(), "k_gmm_resp16_full launch");
         }
-        if (current_opts().gmm_resp16) {
-            const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
-                                                                   : Resp16Shape<128>::LDS);
-            void (*k16)(RespArgs) = d == 64 ? k_gmm_resp16<64> : k_gmm_resp16<128>;
-            static bool attr16 = false;
-            if (!attr16) {
-                (void)hipFuncSetAttribute((const void *)k_gmm_resp16<64>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                (void)hipFuncSetAttribute((const void *)k_gmm_resp16<128>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                attr16 = true;
-            }
-            hipLaunchKernelGGL(k16, dim3((unsigned)((V + 127) / 128)), dim3(256), lds16,
-                               (hipStream_t)stream, a);
-            return hip_error(hipGetLastError(), "k_gmm_resp16 launch");
-        }
-        if (current_opts().gmm_resp_db) {
-            const size_t lds_db = sizeof(float) * (size_t)(d == 64 ? RespDbShape<64>::LDS
-                                                                    : RespDbShape<128>::LDS);
-            // 1 = double-buffered, 2 = + staggered epilogue, 3 = + folded mu_k P_k
-            static void (*const kdbs[3][2])(RespArgs) = {
-                {k_gmm_resp_db<64, 1>, k_gmm_resp_db<128, 1>},
-                {k_gmm_resp_db<64, 2>, k_gmm_resp_db<128, 2>},
-                {k_gmm_resp_db<64, 3>, k_gmm_resp_db<128, 3>}};
-            const int var = current_opts().gmm_resp_db;
-            if (var < 1 || var > 3) return set_error(COME_E_INVALID, "gmm_resp_db must be 0..3");
-            static bool attr_db = false;
-            if (!attr_db) {
-                for (auto &row : kdbs)
-                    for (auto f : row)
-                        (void)hipFuncSetAttribute((const void *)f,
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  160 * 1024);
-                attr_db = true;
-            }
-            hipLaunchKernelGGL(kdbs[var - 1][d == 64 ? 0 : 1], dim3((unsigned)((V + 255) / 256)),
-                               dim3(512), lds_db, (hipStream_t)stream, a);
-            return hip_error(hipGetLastError(), "k_gmm_resp_db launch");
-        }
+        if (r16 != 0)
+            return set_error(COME_E_INVALID, "gmm_resp16 must be 0 or 2 (got %d)", r16);
+        // 0: the 32x32x2 fallback k_gmm_resp_mfma
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(d == 64 ? RespShape<64>::LDS
                                                              : RespShape<128>::LDS);
@@ -2756,25 +2156,19 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
-    const bool cov_async = current_opts().gmm_cov_async != 0;
-    const int cov16 = mfma && current_opts().gmm_cov_async == 3   ? 1
-                      : mfma && current_opts().gmm_cov_async == 4 ? 2
-                                                                   : 0;
-    void (*kern)(CovArgs) =
-        !mfma ? k_gmm_cov_valu
-              : cov16 == 2 ? (d == 64 ? k_gmm_cov16<64, 1> : k_gmm_cov16<128, 1>)
-              : cov16 ? (d == 64 ? k_gmm_cov16<64, 0> : k_gmm_cov16<128, 0>)
-              : cov_async ? (current_opts().gmm_cov_async == 2
-                                 ? (d == 64 ? k_gmm_cov_async<64, 3> : k_gmm_cov_async<128, 3>)
-                                 : (d == 64 ? k_gmm_cov_async<64, 2> : k_gmm_cov_async<128, 2>))
-                            : (d == 64 ? k_gmm_cov_mfma<64> : k_gmm_cov_mfma<128>);
-    const int threads = !mfma        ? 256
-                        : cov16 == 2 ? (d == 64 ? Cov16<64, 1>::THREADS : Cov16<128, 1>::THREADS)
-                        : cov_async  ? CovShape<128>::ATHREADS
-                                    : 64 * (d == 64 ? CovShape<64>::WAVES : CovShape<128>::WAVES);
-    const int cpw = !mfma || !cov_async ? 1
-                    : cov16      ? (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW)
-                                 : (d == 64 ? CovShape<64>::CPW : CovShape<128>::CPW);
+    // gmm_cov_async: 3 (default) = k_gmm_cov16, 1 = the 32x32 fallback k_gmm_cov_async
+    const int cv = current_opts().gmm_cov_async;
+    if (cv != 1 && cv != 3)
+        return set_error(COME_E_INVALID, "gmm_cov_async must be 1 or 3 (got %d)", cv);
+    void (*kern)(CovArgs) = !mfma     ? k_gmm_cov_valu
+                            : cv == 3 ? (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>)
+                                      : (d == 64 ? k_gmm_cov_async<64> : k_gmm_cov_async<128>);
+    const int threads = !mfma     ? 256
+                        : cv == 3 ? (d == 64 ? Cov16<64>::THREADS : Cov16<128>::THREADS)
+                                  : CovShape<128>::ATHREADS;
+    const int cpw = !mfma     ? 1
+                    : cv == 3 ? (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW)
+                              : (d == 64 ? CovShape<64>::CPW : CovShape<128>::CPW);
     hipLaunchKernelGGL(kern, dim3((K + cpw - 1) / cpw, used), dim3(threads), 0,
                        (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 
@@ -79,14 +80,20 @@ static std::unordered_map<void *, Scratch> g_scratch[kMaxDevices][kScratchSlots]
 static std::mutex g_scratch_mu;
 
 
+// Per-(device, slot, stream) scratch that only grows.  A growth is stream-ordered (hipFreeAsync /
+// hipMallocAsync on the stream the scratch serves): the kernels still reading the old buffer on
+// that stream finish first, and no device-wide synchronisation happens in the middle of a stream
+// (a plain hipFree here stalled the device).  Grown by at least 1.5x so a slowly
+// growing caller reallocates O(log) times.
 float *stream_scratch(int device, void *stream, int slot, size_t bytes) {
     if (slot < 0 || slot >= kScratchSlots) return nullptr;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     Scratch &s = g_scratch[device][slot][stream];
     if (s.bytes >= bytes) return s.ptr;
-    if (s.ptr) (void)hipFree(s.ptr);
+    if (s.bytes) bytes = std::max(bytes, s.bytes + s.bytes / 2);
+    if (s.ptr) (void)hipFreeAsync(s.ptr, (hipStream_t)stream);
     s = Scratch{};
-    if (hipMalloc((void **)&s.ptr, bytes) != hipSuccess) {
+    if (hipMallocAsync((void **)&s.ptr, bytes, (hipStream_t)stream) != hipSuccess) {
         s.ptr = nullptr;
         return nullptr;
     }
@@ -153,7 +160,7 @@ extern "C" int come_set_option(const char *name, int value) {
                   COME_OPT(resident_cap),     COME_OPT(community_async),
                   COME_OPT(gmm_cov_async),    COME_OPT(walk_staged),
                   COME_OPT(o2_fresh_loads),   COME_OPT(o2_atomic_writeback),
-                  COME_OPT(gmm_resp_db),      COME_OPT(gmm_resp16),
+                  COME_OPT(gmm_resp16),
                   COME_OPT(o1_chunk)};
 #undef COME_OPT
     for (const auto &f : fields)

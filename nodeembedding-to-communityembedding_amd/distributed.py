@@ -110,13 +110,20 @@ class TorchComm(object):
     def __init__(self, group=None):
         import torch.distributed as dist
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() \
-            else 1
+        up = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if up else 1
+        self.rank = dist.get_rank(group) if up else 0
 
     def all_reduce(self, t, op="sum", async_op=False):
         import torch.distributed as dist
         return dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX,
                                group=self.group, async_op=async_op)
+
+    def broadcast(self, t, src=0):
+        """Blocking broadcast of `t` from group rank `src`."""
+        import torch.distributed as dist
+        gsrc = src if self.group is None else dist.get_global_rank(self.group, src)
+        dist.broadcast(t, gsrc, group=self.group)
 
 
 class LocalReplicas(object):
@@ -131,6 +138,8 @@ class LocalReplicas(object):
         self.world = int(world)
         self.calls = [[] for _ in range(self.world)]
         self.done = 0
+        self.bcast = []
+        self.bcount = [0] * self.world
 
     def comm(self, rank):
         return _LocalComm(self, rank)
@@ -138,13 +147,24 @@ class LocalReplicas(object):
     def _complete(self, k):
         while self.done <= k:
             i = self.done
-            ts = [self.calls[r][i] for r in range(self.world)]
+            ops = [self.calls[r][i] for r in range(self.world)]
+            if len(set(op for op, _ in ops)) != 1:
+                raise RuntimeError("LocalReplicas: ranks disagree on collective %d" % i)
+            ts = [t for _, t in ops]
             acc = ts[0].clone()
             for t in ts[1:]:
-                acc.add_(t)
+                if ops[0][0] == "sum":
+                    acc.add_(t)
+                else:
+                    torch_max(acc, t)
             for t in ts:
                 t.copy_(acc)
             self.done += 1
+
+
+def torch_max(acc, t):
+    import torch
+    torch.maximum(acc, t, out=acc)
 
 
 class _LocalComm(object):
@@ -152,11 +172,24 @@ class _LocalComm(object):
         self.g, self.rank, self.world = group, rank, group.world
 
     def all_reduce(self, t, op="sum", async_op=False):
-        if not async_op or op != "sum":
-            raise NotImplementedError("LocalReplicas: asynchronous SUM all-reduces only")
+        if not async_op or op not in ("sum", "max"):
+            raise NotImplementedError("LocalReplicas: asynchronous SUM / MAX all-reduces only")
         k = len(self.g.calls[self.rank])
-        self.g.calls[self.rank].append(t)
+        self.g.calls[self.rank].append((op, t))
         return _LocalWork(self.g, k)
+
+    def broadcast(self, t, src=0):
+        """The k-th broadcast of every rank forms one collective.  Ranks run in rank order, so
+        `src` = 0 has posted its tensor before the others copy it (a sequential simulation cannot
+        block)."""
+        if src != 0:
+            raise NotImplementedError("LocalReplicas: broadcasts from rank 0 only")
+        k = self.g.bcount[self.rank]
+        self.g.bcount[self.rank] += 1
+        if self.rank == 0:
+            self.g.bcast.append(t.clone())
+        else:
+            t.copy_(self.g.bcast[k])
 
 
 class _LocalWork(object):
@@ -186,44 +219,70 @@ class DeltaAllReduce(object):
     every rank).  ``bucket_elems`` bounds the size of each all-reduce call (large fp32 buckets:
     xGMI collectives are bandwidth-bound per link, so few big calls beat many small ones)."""
 
-    COMBINES = ("sum", "mean", "touched_mean", "hot_mean")
+    COMBINES = ("sum", "mean", "touched_mean", "hot_mean", "pick", "hot_pick")
 
     def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum",
-                 mean_rows=None):
+                 mean_rows=None, pick_rows=None, same_start=True):
         import torch
         if combine not in self.COMBINES:
             raise ValueError("combine must be one of %s" % (self.COMBINES,))
         if combine == "hot_mean" and (mean_rows is None or len(mean_rows) != len(tables)):
             raise ValueError("combine='hot_mean' needs one boolean row mask per table")
+        if combine == "hot_pick" and (pick_rows is None or len(pick_rows) != len(tables)):
+            raise ValueError("combine='hot_pick' needs one boolean row mask per table")
         self.mean_rows = mean_rows
+        self.pick_rows = pick_rows
         self.tables = list(tables)
         self.group = group
         self.comm = comm if comm is not None else TorchComm(group)
         self.world = self.comm.world
+        self.rank = getattr(self.comm, "rank", 0)
         self.bucket = int(bucket_elems)
         self.combine = combine
+        self.exchanges = 0
+        if self.world > 1 and same_start:
+            self._broadcast()
         self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
         self.dsum = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
         self.down = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
         self.cnt = None
+        self.prio = None
+        self.prepared = False
         self.pending = []
 
+    def _broadcast(self):
+        """Every replica starts from rank 0's tables: the exchange adds deltas to each rank's own
+        W_sync, so replicas that started apart (ranks seeded differently) would never meet."""
+        for t in self.tables:
+            self.comm.broadcast(t, 0)
+
     def reset(self):
-        """Make the current tables the sync base (W_sync = W).  Call when every replica holds the
-        same tables but they changed outside the exchange (e.g. another trainer's distributed
-        step), so that change is not counted once per rank as a delta."""
+        """Make the current tables the sync base (W_sync = W), after taking rank 0's tables (the
+        replicas must agree).  Call when the tables changed outside the exchange (e.g. another
+        trainer's distributed step), so that change is not counted once per rank as a delta."""
         self.finish()
         if self.world > 1:
+            self._broadcast()
             for t, s in zip(self.tables, self.snap):
                 s.copy_(t)
 
-    def start(self):
-        """Snapshot this rank's delta and launch its asynchronous all-reduce (finishes any
-        exchange still pending first)."""
-        if self.world == 1:
+    def prepare(self):
+        """First half of start(): finish any pending exchange, snapshot this rank's delta
+        D = W - W_sync and post the per-row flag all-reduces the combine needs (touched_mean: the
+        number of ranks that changed each row; pick: the priority of the rank whose delta a row
+        takes).  start() calls it when it has not run; a one-process simulation of N ranks
+        (LocalReplicas) calls it on every rank before any rank's start()."""
+        if self.world == 1 or self.prepared:
             return
+        import torch
         self.finish()
-        self.cnt = [] if self.combine == "touched_mean" else None
+        count = self.combine in ("touched_mean", "hot_pick")
+        pick = self.combine in ("pick", "hot_pick")
+        self.cnt = [] if count else None
+        self.prio = [] if pick else None
+        # pick: rank (star + j) % N has priority N - j; the star rotates with every exchange
+        star = self.exchanges % self.world
+        mine = self.world - (self.rank - star) % self.world
         for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
             if _fused(t):
                 _native("come_delta_begin", t, s, ds, do)  # D = Down = W - W_sync
@@ -231,29 +290,63 @@ class DeltaAllReduce(object):
                 ds.copy_(t)
                 ds.sub_(s)                                 # D_own = W - W_sync
                 do.copy_(ds)
-            if self.cnt is not None:  # ranks that changed each row (bitwise W != W_sync)
-                c = SparseDeltaAllReduce._flags(t, s)
+            if count or pick:  # the rows this rank changed (bitwise W != W_sync)
+                f = SparseDeltaAllReduce._flags(t, s)
+            if count:
+                c = f.clone()
                 self.cnt.append(c)
                 self.pending.append(self.comm.all_reduce(c, async_op=True))
+            if pick:
+                p = f * mine
+                self.prio.append((p, p.clone()))
+                self.pending.append(self.comm.all_reduce(self.prio[-1][1], op="max",
+                                                         async_op=True))
+        self.prepared = True
+
+    def start(self):
+        """Snapshot this rank's delta and launch its asynchronous all-reduce (finishes any
+        exchange still pending first).  pick / hot_pick wait for the priority all-reduce first
+        (on the device: RCCL's stream, no host block) and zero the rows another rank wins."""
+        if self.world == 1:
+            return
+        self.prepare()
+        self.prepared = False
+        self.exchanges += 1
+        if self.prio is not None:
+            for w in self.pending:
+                w.wait()
+            self.pending = []
+        for i, (t, ds) in enumerate(zip(self.tables, self.dsum)):
+            if self.prio is not None:
+                p, pmax = self.prio[i]
+                lose = (p != pmax) | (p == 0)        # another rank's delta wins this row
+                if self.combine == "hot_pick":
+                    lose &= self.pick_rows[i]
+                ds.masked_fill_(lose.view((-1,) + (1,) * (ds.dim() - 1)), 0.0)
             flat = ds.view(-1)
             for lo in range(0, flat.numel(), self.bucket):
                 hi = min(lo + self.bucket, flat.numel())
                 self.pending.append(self.comm.all_reduce(flat[lo:hi], async_op=True))
+        self.prio = None
 
     def finish(self):
         """Wait for the pending all-reduce (device-side wait on the current stream) and apply
         the other ranks' deltas."""
         if self.world == 1 or not self.pending:
             return
+        if self.prepared:
+            raise RuntimeError("DeltaAllReduce: prepare() without start()")
         for w in self.pending:
             w.wait()
         self.pending = []
         for i, (t, s, ds, do) in enumerate(zip(self.tables, self.snap, self.dsum, self.down)):
             if self.combine == "mean":
                 ds.mul_(1.0 / self.world)
-            elif self.combine == "touched_mean":
-                c = self.cnt[i].clamp_min(1).to(ds.dtype)
-                ds.div_(c.view((-1,) + (1,) * (ds.dim() - 1)))
+            elif self.combine in ("touched_mean", "hot_pick"):
+                c = self.cnt[i].clamp_min(1)
+                if self.combine == "hot_pick":      # picked rows hold one rank's delta
+                    c = c.masked_fill(self.pick_rows[i], 1)
+                ds.div_(c.to(ds.dtype).view((-1,) + (1,) * (ds.dim() - 1)))
             elif self.combine == "hot_mean":  # contended rows averaged, the others summed
                 ds[self.mean_rows[i]] *= 1.0 / self.world
             if _fused(t):
@@ -425,3 +518,20 @@ def reference_touched_mean(w_sync, locals_):
         tot += w.astype(np.float64) - s.astype(np.float64)
         cnt += (w.view(np.int32) != s.view(np.int32)).any(axis=1)
     return out + tot / np.maximum(cnt, 1)[:, None]
+
+
+def reference_pick(w_sync, locals_, star):
+    """Host restatement of one pick sync for tests: a row changed (bitwise) by some rank takes
+    the delta of the first rank in the order star, star + 1, ... (mod N) that changed it; rows
+    nobody changed stay."""
+    s = np.asarray(w_sync, np.float32)
+    out = np.array(s, np.float64, copy=True)
+    n = len(locals_)
+    done = np.zeros(s.shape[0], bool)
+    for j in range(n):
+        w = np.asarray(locals_[(star + j) % n], np.float32)
+        ch = (w.view(np.int32) != s.view(np.int32)).any(axis=1) & ~done
+        out[ch] += w[ch].astype(np.float64) - s[ch].astype(np.float64)
+        done |= ch
+    return out
+

@@ -154,8 +154,10 @@ def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mod
     options (dict of come_launch_opts fields, see include/come.h); update_count: CUDA int64
     tensor [1] that the launch adds its number of applied target-row updates to; hot: the
     contended-row bitmap of hot_rows() (Hogwild mode: those rows are read per pair and updated
-    with float atomics), "auto" (default: derived from `table` by the library per call at
-    DEFAULT_HOT_P) or None (no contended rows: every row updated with plain stores)."""
+    with float atomics), "auto" (default: derived from `table` by the library at DEFAULT_HOT_P
+    before EVERY launch, ~0.1 ms at T = 1e8 -- callers launching many small batches pass
+    Model.hot_rows() instead, as the trainers do) or None (no contended rows: every row updated
+    with plain stores)."""
     import torch
     _require_cuda(node, "node", torch.float32)
     _require_cuda(ctx, "ctx", torch.float32)

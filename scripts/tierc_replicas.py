@@ -81,20 +81,24 @@ def main():
             cname, mrows, lr_r = comb, None, lr
             if cname.endswith("@lrN"):
                 cname, lr_r = cname[:-4], lr * N
-            if cname.startswith("hot_mean"):  # hot_mean[:share] -- rows holding >= share
+            if cname.startswith("hot_"):  # hot_mean / hot_pick[:share] -- rows holding >= share
                 share = float(cname.split(":")[1]) if ":" in cname else tsi.DEFAULT_HOT_P
                 hb = tsi.hot_rows(tab, V, max(1, int(share * len(table))))
                 bits = torch.arange(V, device=dev)
                 mrows = ((hb[bits >> 5] >> (bits & 31)) & 1).bool()
-                cname = "hot_mean"
+                cname = cname.split(":")[0]
+            st = {}
             node, ctx = train_replicas(node0, ctx0, train, seeds, N, min(p, per_rank), w, n,
                                        packed, hot, lr_r, overlap=not args.no_overlap,
-                                       combine=cname, mean_rows=mrows)
+                                       combine=cname,
+                                       mean_rows=mrows if cname == "hot_mean" else None,
+                                       pick_rows=mrows if cname == "hot_pick" else None,
+                                       stats=st)
             l = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
             del node, ctx
             torch.cuda.empty_cache()
             pt = {"world": N, "combine": comb, "sync_walks": min(p, per_rank),
-                  "exchanges": -(-per_rank // min(p, per_rank)), "loss": l,
+                  "exchanges": st.get("exchanges"), "loss": l,
                   "rel_to_seq": (l - fx["seq_loss"]) / fx["seq_loss"], "wall_s": time.time() - t1}
             out["points"].append(pt)
             print(json.dumps(pt), flush=True)

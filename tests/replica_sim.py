@@ -18,8 +18,9 @@ from come_amd.distributed import DeltaAllReduce, LocalReplicas, shard_walks
 
 def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negative, table, hot,
                    lr, alpha=1.0, overlap=True, device="cuda", combine="touched_mean",
-                   mean_rows=None):
-    """Returns (node, ctx) CUDA tensors of replica 0 after the run (all replicas are equal)."""
+                   mean_rows=None, pick_rows=None, stats=None):
+    """Returns (node, ctx) CUDA tensors of replica 0 after the run (all replicas are equal).
+    ``stats``: a dict that receives the number of exchanges each rank made."""
     dev = torch.device(device)
     group = LocalReplicas(world)
     reps, exs, shards = [], [], []
@@ -28,7 +29,8 @@ def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negativ
         c_ = torch.from_numpy(np.ascontiguousarray(ctx0)).to(dev)
         reps.append((n_, c_))
         exs.append(DeltaAllReduce([n_, c_], comm=group.comm(r), combine=combine,
-                                  mean_rows=None if mean_rows is None else [mean_rows] * 2))
+                                  mean_rows=None if mean_rows is None else [mean_rows] * 2,
+                                  pick_rows=None if pick_rows is None else [pick_rows] * 2))
         w, s = shard_walks(walks, seeds, r, world)
         shards.append((torch.from_numpy(np.ascontiguousarray(w, np.int32)).to(dev),
                        torch.from_numpy(np.ascontiguousarray(s, np.uint64).view(np.int64))
@@ -42,16 +44,20 @@ def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negativ
             if wb.shape[0]:
                 tsi.sgns_o2(reps[r][0], reps[r][1], wb.contiguous(), sb.contiguous(), window,
                             negative, table, lr, alpha, tsi.MODE_HOGWILD, hot=hot)
-            if overlap and not last:
-                exs[r].start()  # finishes the previous exchange, launches this one
+        # every rank posts its flag collectives before any rank waits on them (a blocking
+        # wait inside one rank's start() could not complete in a sequential simulation)
+        for e in exs:
+            e.prepare()         # finishes the previous exchange, snapshots this one's delta
+        for e in exs:
+            e.start()           # launches this exchange (overlapped: finished by the next one)
         if overlap and not last:
             continue
         for e in exs:           # blocking exchange = start / finish / settle on every rank
-            e.start()
-        for e in exs:
             e.finish()
             e.settle()
     torch.cuda.synchronize(dev)
     for r in range(1, world):
         assert torch.equal(reps[r][0], reps[0][0]) and torch.equal(reps[r][1], reps[0][1])
+    if stats is not None:
+        stats["exchanges"] = exs[0].exchanges
     return reps[0]

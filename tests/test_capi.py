@@ -26,7 +26,19 @@ def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.come_abi_version() == _lib.ABI_VERSION == 2
+    assert L.come_abi_version() == _lib.ABI_VERSION == 3
+
+
+def test_library_is_the_build_of_the_sources_beside_it(monkeypatch):
+    """libcome.so carries the SHA-256 of the sources it was built from; the binding compares it
+    with the sources in the tree and refuses a stale library (the prebuilt .so that travels to the
+    GPU box is therefore the committed sources' build)."""
+    L = _lib.lib()
+    assert L.come_source_sha256().decode() == _lib.source_sha256()
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "source_sha256", lambda: "0" * 64)
+    with pytest.raises(_lib.ComeError, match="built from other sources"):
+        _lib.lib()
 
 
 def test_invalid_arguments_return_error_without_gpu():
@@ -79,7 +91,7 @@ def test_launch_options_snapshot_and_per_call_struct():
         _lib.set_option("no_such_knob", 1)
     with pytest.raises(ValueError):
         _lib.launch_opts(no_such_knob=1)
-    assert ctypes.sizeof(_lib.LaunchOpts) == 17 * 4 + 4 + 8  # 17 ints, padding, the pointer
+    assert ctypes.sizeof(_lib.LaunchOpts) == 16 * 4 + 8  # 16 ints, the pointer
     p = ctypes.c_void_p(0)
     rc = L.come_sgns_o2_ex(p, p, 0, 128, p, 1, 10, p, 5, 5, p, 10, 0.1, 1.0, 0, p,
                            ctypes.byref(o), p)

@@ -176,3 +176,93 @@ def test_touched_mean_world2_dense_and_sparse(tmp_path):
         np.testing.assert_allclose(r0[:10], locs[0][:10], rtol=0, atol=1e-6)  # one rank: full
         res.append(r0)
     np.testing.assert_allclose(res[0], res[1], rtol=0, atol=1e-6)
+
+
+def test_pick_three_local_replicas_rotates_the_winner():
+    """combine='pick' (the SGNS trainers' exchange) on three ranks simulated in one
+    process (distributed.LocalReplicas): a row changed by one rank takes its full delta, a row
+    changed by several takes the delta of the first of them in the rotating order star, star + 1,
+    ... (star = exchange index mod N), unchanged rows stay; every replica ends equal; the ranks
+    start from rank 0's tables whatever they held (the exchange broadcasts them)."""
+    from come_amd.distributed import LocalReplicas, reference_pick
+    W, V, d = 3, 12, 4
+    g = LocalReplicas(W)
+    base = torch.randn(V, d)
+    tabs = [base.clone() + (0 if r == 0 else 7.0 * r) for r in range(W)]  # seeded apart
+    exs = [DeltaAllReduce([tabs[r]], comm=g.comm(r), combine="pick") for r in range(W)]
+    for t in tabs:
+        assert torch.equal(t, base)
+    rng = np.random.RandomState(5)
+    for ex_i in range(4):
+        w_sync = tabs[0].numpy().copy()
+        for r in range(W):  # rank r changes rows r .. r + 5 (overlaps) and one row alone
+            tabs[r][r:r + 6] += torch.from_numpy(rng.randn(6, d).astype(np.float32))
+            tabs[r][9 + r] -= 1.0
+        locs = [t.numpy().copy() for t in tabs]
+        for e in exs:
+            e.prepare()
+        for e in exs:
+            e.start()
+        for e in exs:
+            e.finish()
+            e.settle()
+        for t in tabs[1:]:
+            assert torch.equal(t, tabs[0])
+        ref = reference_pick(w_sync, locs, ex_i % W)
+        np.testing.assert_allclose(tabs[0].numpy(), ref, rtol=0, atol=1e-5)
+        np.testing.assert_array_equal(tabs[0].numpy()[9 + 0], locs[0][9])  # one rank: its row
+        star = ex_i % W
+        np.testing.assert_allclose(tabs[0].numpy()[5], locs[star][5], rtol=0, atol=1e-6)
+
+
+def _worker_pick(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.RandomState(10 + rank)   # every rank seeded differently
+    t = torch.from_numpy(rng.randn(41, 8).astype(np.float32))
+    sync = DeltaAllReduce([t], combine="pick", bucket_elems=64)
+    np.save(os.path.join(out_dir, "start%d.npy" % rank), t.numpy().copy())
+    for step in range(3):
+        w_sync = t.numpy().copy()
+        lo, hi = (0, 20) if rank == 0 else (10, 30)
+        t[lo:hi] += torch.from_numpy(np.random.RandomState(7 + rank + 10 * step)
+                                     .randn(hi - lo, 8).astype(np.float32))
+        np.save(os.path.join(out_dir, "sync%d_%d.npy" % (step, rank)), w_sync)
+        np.save(os.path.join(out_dir, "loc%d_%d.npy" % (step, rank)), t.numpy().copy())
+        if step == 1:      # overlapped: progress during the exchange is kept
+            sync.start()
+            t[35] += 1.0 + rank
+            sync.finish()
+            sync.sync()
+        else:
+            sync.sync()
+        np.save(os.path.join(out_dir, "res%d_%d.npy" % (step, rank)), t.numpy().copy())
+    dist.destroy_process_group()
+
+
+def test_pick_world2_from_differently_seeded_ranks(tmp_path):
+    """combine='pick' over a real process group (gloo, world 2): the replicas start from rank 0's
+    table although the ranks were seeded differently, rows changed by both ranks take
+    the rotating winner's delta (rank 0 at exchange 0, rank 1 at exchange 1, ...), rows changed by
+    one rank its full delta, and the replicas agree after every exchange; progress made during an
+    overlapped exchange lands on top."""
+    from come_amd.distributed import reference_pick
+    mp.spawn(_worker_pick, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    ld = lambda n: np.load(str(tmp_path / n))  # noqa: E731
+    np.testing.assert_array_equal(ld("start0.npy"), ld("start1.npy"))
+    np.testing.assert_array_equal(ld("start0.npy"), np.random.RandomState(10).randn(41, 8)
+                                  .astype(np.float32))
+    ex = 0
+    for step in range(3):
+        r0, r1 = ld("res%d_0.npy" % step), ld("res%d_1.npy" % step)
+        np.testing.assert_array_equal(r0, r1)
+        locs = [ld("loc%d_%d.npy" % (step, r)) for r in range(2)]
+        ref = reference_pick(ld("sync%d_0.npy" % step), locs, ex % 2)
+        np.testing.assert_allclose(r0[:30], ref[:30], rtol=0, atol=1e-5)
+        if step >= 1:   # row 35, changed by both ranks during exchange 1, synced by exchange 2
+            np.testing.assert_allclose(r0[35], ld("start0.npy")[35] + 1.0, rtol=0, atol=1e-6)
+        if step == 1:   # (star 0 wins exchange 2: rank 0's +1)
+            ex += 1
+        np.testing.assert_array_equal(r0[30:35], ld("sync%d_0.npy" % step)[30:35])
+        ex += 1

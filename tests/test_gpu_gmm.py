@@ -81,18 +81,14 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("variant", [0, 3, "16", "16t", "16t0"])
-def test_estep_mixed_factor_shapes(d, variant):
+@pytest.mark.parametrize("r16", [0, 2])
+def test_estep_mixed_factor_shapes(d, r16):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
-    loop.  Mixed in one launch, every component must match the float64 quadratic form -- for
-    k_gmm_resp_mfma (variant 0), the staggered double-buffered kernel whose accumulators start
-    at -mu_k P_k (gmm_resp_db = 3) and the 16x16x4 kernel k_gmm_resp16 (gmm_resp16 = 1; a lower
-    or dense factor in the launch makes it run every block of every component), and its packed
-    form k_gmm_resp16t: the default one-row-tile variant (gmm_resp16 = 2), whose FULL case is
-    the separate k_gmm_resp16_full launch, and the two-row-tile one (= 16), which holds the
-    FULL body itself."""
-    from come_amd import _lib
+    loop.  Mixed in one launch, every component must match the float64 quadratic form -- for the
+    default k_gmm_resp16t (gmm_resp16 = 2: a lower or dense factor in the launch sends every
+    component to the separate k_gmm_resp16_full launch) and the 32x32 fallback k_gmm_resp_mfma
+    (gmm_resp16 = 0: per-component flags)."""
     V, K = 1500, 6
     rng = np.random.RandomState(d)
     X = rng.standard_normal((V, d)).astype(np.float32)
@@ -107,8 +103,7 @@ def test_estep_mixed_factor_shapes(d, variant):
     ln = np.log(np.full(K, 1.0 / K))
     mp = np.einsum("kd,kde->ke", mu.astype(np.float64), P)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
-    r16 = {"16": 1, "16t": 2, "16t0": 16}.get(variant, 0)
-    with opts(gmm_resp16=r16, gmm_resp_db=0 if r16 else variant):
+    with opts(gmm_resp16=r16):
         resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
     Y = np.einsum("vd,kde->vke", X.astype(np.float64), P) - mp[None]
     lp = ln[None] - 0.5 * (Y ** 2).sum(-1)
@@ -120,10 +115,10 @@ def test_estep_mixed_factor_shapes(d, variant):
 
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (70_001, 7, 64), (300, 3, 64), (129, 1, 128),
                                    (1, 4, 128), (5000, 2, 128)])
-def test_estep16t_variants_bit_identical(V, K, d):
-    """k_gmm_resp16t's wave shapes change no arithmetic: two row tiles per wavefront (gmm_resp16 =
-    16, VT 0) equals one (the default 2 = VT 8) bit for bit, and so do the packed-fp32-epilogue
-    forms (17, VT 2 and 19, VT 10), ragged row counts included."""
+def test_estep_default_and_fallback_agree(V, K, d):
+    """The default E-step (k_gmm_resp16t, 16-wide blocks) and the 32x32 fallback
+    (k_gmm_resp_mfma) on sklearn-shaped upper factors, ragged row counts: the same quantities
+    summed in different orders -- equal to float tolerance, responsibilities summing to 1."""
     rng = np.random.RandomState(V + 7 * K)
     X = rng.standard_normal((V, d)).astype(np.float32)
     P = np.stack([np.triu(rng.standard_normal((d, d)) / np.sqrt(d)) + 2 * np.eye(d)
@@ -133,21 +128,46 @@ def test_estep16t_variants_bit_identical(V, K, d):
     ln = np.log(rng.dirichlet(np.ones(K)))
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
     out = {}
-    for r16 in (16, 2, 17, 19):
+    for r16 in (2, 0):
         with opts(gmm_resp16=r16):
             resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
         out[r16] = resp.cpu().numpy(), lse.cpu().numpy()
-    for a, b in ((2, 16), (19, 17)):
-        np.testing.assert_array_equal(out[a][0], out[b][0])
-        np.testing.assert_array_equal(out[a][1], out[b][1])
     assert np.isfinite(out[2][0]).all() and np.abs(out[2][0].sum(1) - 1).max() < 1e-4
-    np.testing.assert_allclose(out[19][0], out[2][0], atol=1e-4)  # own rounding: even/odd sums
+    np.testing.assert_allclose(out[2][0], out[0][0], atol=1e-4)
+    np.testing.assert_allclose(out[2][1], out[0][1], rtol=1e-5, atol=1e-3)
+
+
+def test_variant_options_outside_the_kept_set_are_rejected():
+    """The launch options that pick a GMM / community kernel accept only the default and its one
+    fallback (include/come.h); any other value fails the call with COME_E_INVALID instead of
+    silently running some other kernel."""
+    from come_amd import _lib
+    from come_amd import community_embeddings as ce
+    d, K, V = 128, 3, 200
+    rng = np.random.RandomState(3)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
+    X = t(rng.standard_normal((V, d)))
+    P = t(np.stack([np.eye(d)] * K))
+    mp, ln = t(np.zeros((K, d))), t(np.log(np.full(K, 1.0 / K)))
+    R = t(rng.dirichlet(np.ones(K), V))
+    for bad in (1, 3, 7, 16, 19):
+        with opts(gmm_resp16=bad):
+            with pytest.raises(_lib.ComeError, match="gmm_resp16"):
+                gmm.estep(X, P, mp, ln)
+    for bad in (0, 2, 4):
+        with opts(gmm_cov_async=bad):
+            with pytest.raises(_lib.ComeError, match="gmm_cov_async"):
+                gmm.scatter(X, R, mp)
+    for bad in (0, 3):
+        with opts(community_async=bad):
+            with pytest.raises(_lib.ComeError, match="community_async"):
+                ce.community_grad(X.clone(), R, mp, P, 0.01, 0.1, 1)
 
 
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
                                           (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None),
                                           (1500, 3, 256, 4), (200, 2, 330, None)])
-@pytest.mark.parametrize("cov", [1, 3, 4])
+@pytest.mark.parametrize("cov", [1, 3])
 def test_scatter_vs_numpy(V, K, d, chunks, cov):
     rng = np.random.RandomState(V + K)
     X = rng.normal(size=(V, d)).astype(np.float32)
@@ -245,26 +265,24 @@ def test_community2vec_distributed_flag_single_process_matches():
 @pytest.mark.parametrize("V,K,d,chunks", [(4097, 5, 128, 7), (999, 3, 128, None),
                                           (5000, 3, 64, None), (65, 4, 64, 2), (700, 1, 128, 3),
                                           (517, 7, 64, 2), (1031, 9, 64, None)])
-def test_scatter_async_matches_sync(V, K, d, chunks):
-    """k_gmm_cov_async (2 (d=128) / 4 (d=64) components per workgroup, operands centred and
-    weighted once per block into transposed LDS images, the same fp32 products) and k_gmm_cov16
-    (the same on 16x16x4 tiles, gmm_cov_async = 3; 4: its tiles over twice the wavefronts, bit-
-    identical to 3) against the synchronous k_gmm_cov_mfma: equal
-    up to the order the MFMAs accumulate the samples in (atol 1e-5 of the matrix scale).  K not a
-    multiple of the components per workgroup included."""
-    from come_amd import _lib
+def test_scatter_default_and_fallback_agree(V, K, d, chunks):
+    """k_gmm_cov16 (default, 16x16x4 tiles) and the 32x32 fallback k_gmm_cov_async (2 (d=128) / 4
+    (d=64) components per workgroup, operands centred and weighted once per block into
+    transposed LDS images, the same fp32 products): equal up to the order the MFMAs accumulate
+    the samples in (atol 1e-5 of the matrix scale), exactly symmetric.  K not a multiple of the
+    components per workgroup included."""
     rng = np.random.RandomState(V + K + d)
     t = lambda a: torch.as_tensor(a, device=dev())  # noqa: E731
     x = t(rng.standard_normal((V, d)).astype(np.float32))
     resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
     mu = t(rng.standard_normal((K, d)).astype(np.float32))
     out = []
-    for opt in (0, 1, 2, 3, 4):  # sync; async with 2 image buffers / with 3; 16x16x4 tiles;
-        with opts(gmm_cov_async=opt):  # 16x16x4 with twice the MFMA wavefronts
+    for opt in (3, 1):
+        with opts(gmm_cov_async=opt):
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
-    for o in out[1:]:
-        np.testing.assert_allclose(o, out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
-    np.testing.assert_array_equal(out[4], out[3])  # the same per-tile sample order
+    np.testing.assert_allclose(out[1], out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
+    for o in out:
+        np.testing.assert_array_equal(o, np.swapaxes(o, 1, 2))
 
 
 def test_community2vec_trains_at_d256():
@@ -292,47 +310,13 @@ def test_community2vec_trains_at_d256():
         np.testing.assert_allclose(m.node_embedding.cpu().numpy(), ref, rtol=2e-5, atol=2e-5)
 
 
-@pytest.mark.parametrize("V,K,d", [(1000, 5, 128), (4097, 50, 128), (300, 3, 64), (2049, 9, 64),
-                                   (257, 1, 128)])
-def test_estep_double_buffered_kernel_bit_identical(V, K, d):
-    """k_gmm_resp_db (gmm_resp_db=1: one 8-wavefront workgroup per CU, P_{k+1} staged into the
-    second LDS buffer while component k computes; =2: the second wave of each SIMD runs every
-    epilogue one component late) against k_gmm_resp_mfma: the same MFMA order per column tile and
-    the same epilogue -> bit-identical responsibilities and log-sum-exp, with upper, lower and
-    dense factors mixed and ragged row counts.  =3 (accumulators start at -mu_k P_k) rounds
-    differently: checked to float tolerance against the others."""
-    from come_amd import _lib
-    rng = np.random.RandomState(V + K + d)
-    X = rng.standard_normal((V, d)).astype(np.float32)
-    P = []
-    for k in range(K):
-        A = rng.standard_normal((d, d)) / np.sqrt(d)
-        P.append(np.triu(A) + 2 * np.eye(d) if k % 3 == 0 else
-                 np.tril(A) + 2 * np.eye(d) if k % 3 == 1 else A + 2 * np.eye(d))
-    P = np.stack(P).astype(np.float32)
-    mp = rng.standard_normal((K, d)).astype(np.float32)
-    ln = np.log(rng.dirichlet(np.ones(K))).astype(np.float32)
-    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev())  # noqa: E731
-    out = []
-    for opt in (0, 1, 2, 3):
-        with opts(gmm_resp16=0, gmm_resp_db=opt):
-            r, l = gmm.estep(t(X), t(P), t(mp), t(ln))
-        out.append((r.cpu().numpy(), l.cpu().numpy()))
-    for o in out[1:3]:
-        np.testing.assert_array_equal(out[0][0], o[0])
-        np.testing.assert_array_equal(out[0][1], o[1])
-    np.testing.assert_allclose(out[3][0], out[0][0], rtol=1e-4, atol=1e-6)
-    np.testing.assert_allclose(out[3][1], out[0][1], rtol=1e-5, atol=1e-4)
-
-
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (1000, 5, 128), (2049, 9, 64), (300, 3, 64),
                                    (129, 1, 128)])
-@pytest.mark.parametrize("r16", [1, 2, 16, 17, 19])
-def test_estep16_upper_factors_vs_float64(V, K, d, r16):
-    """k_gmm_resp16 (gmm_resp16 = 1) and its packed one-barrier form k_gmm_resp16t (= 2) with
-    sklearn-shaped (upper-triangular) precision factors only -- the launches that take the 16-wide
+@pytest.mark.parametrize("r16", [0, 2])
+def test_estep_upper_factors_vs_float64(V, K, d, r16):
+    """The default k_gmm_resp16t (gmm_resp16 = 2) and the fallback k_gmm_resp_mfma (= 0) with
+    sklearn-shaped (upper-triangular) precision factors only -- the launches that take the
     triangular skip -- against the float64 quadratic form, ragged rows."""
-    from come_amd import _lib
     from scipy.special import logsumexp
     rng = np.random.RandomState(V + K)
     X = rng.standard_normal((V, d)).astype(np.float32)

@@ -369,10 +369,13 @@ def test_community_grad_vs_golden():
                                    err_msg=name)
 
 
-@pytest.mark.parametrize("d,V,K,iters", [(64, 1000, 7, 3), (128, 777, 5, 2), (128, 300, 1, 1),
-                                          (96, 200, 3, 2), (256, 150, 3, 2), (500, 37, 2, 1),
-                                          (128, 4097, 4, 2), (64, 129, 3, 1)])
-@pytest.mark.parametrize("kern", [1, 2])
+_MFMA_COMM = [(64, 1000, 7, 3), (128, 777, 5, 2), (128, 300, 1, 1), (128, 4097, 4, 2),
+              (64, 129, 3, 1)]
+_VALU_COMM = [(96, 200, 3, 2), (256, 150, 3, 2), (500, 37, 2, 1)]
+
+
+@pytest.mark.parametrize("d,V,K,iters,kern", [c + (k,) for c in _MFMA_COMM for k in (1, 2)] +
+                         [c + (2,) for c in _VALU_COMM])
 def test_community_grad_vs_oracle(d, V, K, iters, kern):
     """MFMA path (d = 64, 128; ragged row tiles; community_async = 1: k_community_async on
     32x32x2 MFMAs, 2: k_community16 on 16x16x4 with one row tile per wavefront), VALU path
@@ -380,8 +383,6 @@ def test_community_grad_vs_oracle(d, V, K, iters, kern):
     numpy restatement of community_embeddings.py:61-78: fp32 contractions in another order,
     rtol/atol 2e-5; the clip at +-5 is exercised (beta large)."""
     from come_amd import _lib
-    if kern == 2 and d not in (64, 128):
-        pytest.skip("k_community16 serves d = 64, 128")
     prev = _lib.launch_opts().community_async
     _lib.set_option("community_async", kern)
     try:
