@@ -68,14 +68,19 @@ def cpu_port_baseline(walks_np, seeds_np, node_np, ctx_np, table_np, window, neg
 
 def secondary_rows(timeout_s=150):
     """The other hot-path rows measured on the same GPU after the timed region, each by
-    bench_aux.py in a child process (one JSON line each; CPU baselines skipped): C2 O1 pass,
-    C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass.  Outside the
-    timed region and never part of `value`; a failing row is reported as an error string."""
+    bench_aux.py in a child process (one JSON line each, with its bounded CPU baseline: the O1
+    Hogwild restatement for ~6 s plus its reference-equivalent rate, the reference's numpy
+    community loop and one sklearn EM iteration on row samples; none for the walker):
+    C2 O1 pass, C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass.
+    Outside the timed region and never part of `value`; a failing row is reported as an error
+    string."""
     import subprocess
     out = {}
     for wl in ("c2", "c4", "walks"):
         cmd = [sys.executable, os.path.join(ROOT, "bench_aux.py"), "--workload", wl,
-               "--steps", "10", "--warmup", "2", "--no-cpu-baseline"]
+               "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]
+        if wl == "walks":  # its baseline walks a full corpus pass per thread (~20 s): skipped
+            cmd.append("--no-cpu-baseline")
         t0 = time.time()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
@@ -87,7 +92,8 @@ def secondary_rows(timeout_s=150):
             row = {"metric": j["metric"], "value": j["value"], "unit": j["unit"],
                    "ms_per_step": j["ms_per_step"], "workload": j["config"]["workload"],
                    "roofline_frac": j["roofline"]["frac"], "roofline_bound": j["roofline"]["bound"],
-                   "avg_kernel_ms": j["roofline"]["avg_kernel_ms"], "wall_s": time.time() - t0}
+                   "avg_kernel_ms": j["roofline"]["avg_kernel_ms"], "wall_s": time.time() - t0,
+                   "cpu_baseline": j.get("cpu_baseline")}
             if wl == "c4":
                 for k in ("gmm_resp_kernel", "gmm_resp_ms", "gmm_resp_tflops_executed",
                           "gmm_scatter_ms",

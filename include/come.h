@@ -254,7 +254,8 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       wavefronts in flight so updates stay sparse on small vocabularies
  *                       (defaults 16 / 12; 0 = no cap)
  *   max_waves           absolute cap on wavefronts in flight (0 = none)
- *   o1_blocks_per_cu    O1 grid cap in 4-wave workgroups per CU (0 = 6)
+ *   o1_blocks_per_cu    O1 grid cap in 4-wave workgroups per CU (0 = 8 for the run kernel at
+ *                       d <= 128, n <= 5 -- compiled for 8 waves per SIMD there -- else 6)
  *   resident_cap        1 = also clamp grids to the workgroups the occupancy API reports resident
  *   community_async     community gradient at d = 64, 128 (16-B aligned mu / inv_cov; else the
  *                       VALU kernel): default 2 = k_community16 (16x16x4 MFMAs, one 16-row tile

@@ -21,6 +21,14 @@
 namespace come {
 
 constexpr int kTR = 16;        // rows per workgroup tile
+
+// A/B hook (scripts/build_ab.sh ... -DCOME_AB_PRIO): raise the wave priority over the MFMA
+// clusters of the 16x16x4 kernels (MI355X guide T5); off in the product build.
+#ifdef COME_AB_PRIO
+#define COME_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define COME_PRIO(x) ((void)0)
+#endif
 constexpr int kThreads = 256;
 
 // out[r][c] = sum_j A[r][j] * B(c, j) for the tile, where B(c, j) = Bm[c*d + j] (TRANS=false,
@@ -412,6 +420,7 @@ __device__ __forceinline__ void comm16_phase(const __attribute__((ext_vector_typ
     f32x4 av[3];
     av[0] = fetch(0);
     av[1] = fetch(1);
+    COME_PRIO(1);
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
         if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
@@ -421,6 +430,7 @@ __device__ __forceinline__ void comm16_phase(const __attribute__((ext_vector_typ
             acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], bq[qq][t], acc[ct], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
+    COME_PRIO(0);
 }
 
 template <int D>
@@ -1087,6 +1097,7 @@ __device__ __forceinline__ void r16t_blocks(
     f32x4 av[3];
     av[0] = fetch(0);
     av[1] = fetch(1);
+    COME_PRIO(1);
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
         if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
@@ -1096,6 +1107,7 @@ __device__ __forceinline__ void r16t_blocks(
             acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[q][t], acc[ct], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
+    COME_PRIO(0);
 }
 
 // log N(x_row; mu_k, P_k) of the lane's row for the component in `buf`
@@ -1163,18 +1175,23 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
     __syncthreads();
     const int64_t my_row = row0 + j16;  // lanes 0-15 own the tile's rows
     const bool owner = kg == 0 && my_row < a.V;
-    float run_max = -INFINITY, run_sum = 0.0f;
+    float run_max = -INFINITY, run_sum = 0.0f, lp_prev = 0.0f;
     for (int k = 0; k < a.K; ++k) {
         const float *buf = sm + (k & 1) * T::BUF;
         if (k + 1 < a.K) r16t_stage<D>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
+        // component k - 1's log-probability is stored one component late: a store counts on the
+        // vector-memory counter like the staging copies, so storing it right before the barrier's
+        // vmcnt(0) made every wavefront wait out the store's round trip once per component
+        if (k > 0 && owner) a.resp[my_row * a.K + k - 1] = lp_prev;
         const float lp = r16t_lp<D>(xb, buf, abase, kg);
-        if (owner) a.resp[my_row * a.K + k] = lp;
         lse_push(lp, run_max, run_sum);
+        lp_prev = lp;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
     }
     if (owner) {
         float *lp = a.resp + my_row * a.K;
+        lp[a.K - 1] = lp_prev;
         const float lse = run_max + logf(run_sum);
         for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
         if (a.lse) a.lse[my_row] = lse;
@@ -1583,6 +1600,7 @@ __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, 
     const int j16 = lane & 15, kg = lane >> 4;
     for (int j = 0; j < nb; ++j) {
         __syncthreads();  // barrier j: block j staged
+        COME_PRIO(1);
         const float *buf = img + (j % C::NBUF) * C::BUF;
         const float *im = buf + tk * C::IMG;
 #pragma unroll
@@ -1610,6 +1628,7 @@ __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, 
                 if (n + 1 < C::NTW && TT.ct[P][n + 1] != TT.ct[P][n]) cur ^= 1;
             }
         }
+        COME_PRIO(0);
     }
 }
 

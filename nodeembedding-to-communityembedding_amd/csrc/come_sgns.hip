@@ -223,7 +223,10 @@ extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edg
         rc = derive_hot_rows(dev, table, T, packed, V, stream, &hot_rows);
         if (rc) return rc;
     }
-    const int bpc = o.o1_blocks_per_cu > 0 ? o.o1_blocks_per_cu : 6;
+    // default grid: 8 four-wave workgroups per CU where the run kernel is compiled for 8 waves per
+    // SIMD (d <= 128, n <= 5: o1_runs_waves_per_eu), else 6
+    const int bpc = o.o1_blocks_per_cu > 0 ? o.o1_blocks_per_cu
+                    : (o.o1_chunk != 0 && d <= 128 && negative <= 5) ? 8 : 6;
     const int64_t hcap = mode == COME_MODE_HOGWILD ? hog_max_blocks(o, V, 4, o.o1_rows_per_wave) : 0;
     int64_t chunk = o.o1_chunk;
     if (chunk < 0) {  // auto: one contiguous chunk per wavefront of the grid

@@ -1272,8 +1272,20 @@ __global__ void __launch_bounds__(256) k_sgns_o1(O1Args a) {
 // it back once when u changes or the chunk ends: a float-atomic delta of the run's updates if u is
 // contended, else a plain store.  Any target row equal to the held u is taken from the registers.
 // One wavefront in sequential mode: bit-identical to k_sgns_o1 (the held row is what memory holds).
+// Wavefronts per SIMD the run kernel is compiled for: latency-bound like the stream kernel (one
+// edge's rows in flight per wavefront), so at d <= 128, n <= 5 it is held to 64 VGPRs (a 12-byte
+// prologue spill) for 8 waves per SIMD and launched 8 four-wave workgroups per CU: C2 at lr 0.1
+// 1.161 vs 1.277 ms per pass at its natural 79 VGPRs / 6 waves (7 waves: 1.186 ms;
+// profiles/r05_ab_o1_waves.txt).
+template <int VEC, int MAXN>
+constexpr int o1_runs_waves_per_eu() {
+    return (VEC <= 2 && MAXN <= 5) ? 8 : 1;
+}
+
 template <int VEC, bool FULL, int MAXN>
-__global__ void __launch_bounds__(256) k_sgns_o1_runs(O1Args a) {
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu(o1_runs_waves_per_eu<VEC, MAXN>())))
+    k_sgns_o1_runs(O1Args a) {
     using R = Row<VEC, FULL>;
     const int lane = threadIdx.x & 63;
     const int64_t waves_per_block = blockDim.x >> 6;

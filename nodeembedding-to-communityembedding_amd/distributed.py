@@ -281,6 +281,8 @@ class DeltaAllReduce(object):
         self.cnt = [] if count else None
         self.prio = [] if pick else None
         # pick: rank (star + j) % N has priority N - j; the star rotates with every exchange
+        if pick and self.world > 127:
+            raise ValueError("combine='pick' supports at most 127 ranks (uint8 priorities)")
         star = self.exchanges % self.world
         mine = self.world - (self.rank - star) % self.world
         for t, s, ds, do in zip(self.tables, self.snap, self.dsum, self.down):
@@ -297,7 +299,12 @@ class DeltaAllReduce(object):
                 self.cnt.append(c)
                 self.pending.append(self.comm.all_reduce(c, async_op=True))
             if pick:
-                p = f * mine
+                # A rank whose change of a row is rounding-level only (an overlapped exchange
+                # leaves W_sync + D_own one rounding away from W on rows nobody else changed) must
+                # not win the row over a rank that trained it: such keys carry bit 7 clear.
+                v = ds.reshape(ds.shape[0], -1)
+                real = v.abs().amax(dim=1) > s.reshape(s.shape[0], -1).abs().amax(dim=1) * 2.0 ** -20
+                p = f * (mine + 128 * real.to(torch.uint8))
                 self.prio.append((p, p.clone()))
                 self.pending.append(self.comm.all_reduce(self.prio[-1][1], op="max",
                                                          async_op=True))

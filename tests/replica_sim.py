@@ -61,3 +61,47 @@ def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negativ
     if stats is not None:
         stats["exchanges"] = exs[0].exchanges
     return reps[0]
+
+
+def train_replicas_o1(node0, edges, seeds_per_pass, world, sync_edges, negative, table, hot, lr,
+                      device="cuda", combine="pick", stats=None):
+    """N ranks of Node2Vec(distributed=True).train (node_embeddings.py) in one process: every pass
+    each rank trains its contiguous shard of the edge list (distributed.shard_range) in launches
+    of ``sync_edges`` edges (None = the whole shard), each followed by the trainer's blocking
+    exchange of node_embedding (DeltaAllReduce, RCCL replaced by LocalReplicas).
+    seeds_per_pass: list of uint64 [E] arrays, one per pass (every rank draws every edge's seed).
+    Returns the node table (a CUDA tensor; all replicas equal)."""
+    from come_amd.distributed import shard_range
+    dev = torch.device(device)
+    group = LocalReplicas(world)
+    reps, exs = [], []
+    for r in range(world):
+        n_ = torch.from_numpy(np.ascontiguousarray(node0)).to(dev)
+        reps.append(n_)
+        exs.append(DeltaAllReduce([n_], comm=group.comm(r), combine=combine))
+    ed = torch.from_numpy(np.ascontiguousarray(edges, np.int32)).to(dev)
+    E = ed.shape[0]
+    for seeds in seeds_per_pass:
+        sd = torch.from_numpy(np.ascontiguousarray(seeds, np.uint64).view(np.int64)).to(dev)
+        biggest = shard_range(E, 0, world)[1]
+        per = sync_edges or max(1, biggest)
+        for b in range(max(1, -(-biggest // per))):
+            for r in range(world):
+                lo, hi = shard_range(E, r, world)
+                s, e = min(hi, lo + b * per), min(hi, lo + (b + 1) * per)
+                if e > s:
+                    tsi.sgns_o1(reps[r], ed[s:e], sd[s:e], negative, table, lr, tsi.MODE_HOGWILD,
+                                hot=hot)
+            for x in exs:       # Node2Vec's exchange is blocking (ex.sync())
+                x.prepare()
+            for x in exs:
+                x.start()
+            for x in exs:
+                x.finish()
+                x.settle()
+    torch.cuda.synchronize(dev)
+    for r in range(1, world):
+        assert torch.equal(reps[r], reps[0])
+    if stats is not None:
+        stats["exchanges"] = exs[0].exchanges
+    return reps[0]

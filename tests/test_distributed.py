@@ -266,3 +266,30 @@ def test_pick_world2_from_differently_seeded_ranks(tmp_path):
             ex += 1
         np.testing.assert_array_equal(r0[30:35], ld("sync%d_0.npy" % step)[30:35])
         ex += 1
+
+
+def test_pick_real_change_beats_rounding_level_change():
+    """An overlapped exchange can leave W_sync + D_own one rounding away from W on a row nobody
+    changed since; such a row must not win over a rank that trained it, whatever the rotation:
+    keys of rounding-level deltas rank below every real change."""
+    from come_amd.distributed import LocalReplicas
+    W, V, d = 3, 6, 8
+    g = LocalReplicas(W)
+    base = torch.randn(V, d) + 3.0
+    tabs = [base.clone() for _ in range(W)]
+    exs = [DeltaAllReduce([tabs[r]], comm=g.comm(r), combine="pick") for r in range(W)]
+    # exchange 0: star = rank 0.  Rank 0 nudges row 2 by one ulp (rounding-level), rank 2 trains it
+    tabs[0][2] = torch.nextafter(tabs[0][2], tabs[0][2] + 1.0)
+    tabs[2][2] += 0.5
+    tabs[1][4] = torch.nextafter(tabs[1][4], tabs[1][4] + 1.0)  # rounding-level, nobody else
+    for e in exs:
+        e.prepare()
+    for e in exs:
+        e.start()
+    for e in exs:
+        e.finish()
+        e.settle()
+    np.testing.assert_allclose(tabs[0][2].numpy(), base[2].numpy() + 0.5, rtol=1e-6)
+    assert torch.equal(tabs[0][4], torch.nextafter(base[4], base[4] + 1.0))  # still taken
+    for t in tabs[1:]:
+        assert torch.equal(t, tabs[0])

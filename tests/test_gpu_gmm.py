@@ -269,8 +269,10 @@ def test_scatter_default_and_fallback_agree(V, K, d, chunks):
     """k_gmm_cov16 (default, 16x16x4 tiles) and the 32x32 fallback k_gmm_cov_async (2 (d=128) / 4
     (d=64) components per workgroup, operands centred and weighted once per block into
     transposed LDS images, the same fp32 products): equal up to the order the MFMAs accumulate
-    the samples in (atol 1e-5 of the matrix scale), exactly symmetric.  K not a multiple of the
-    components per workgroup included."""
+    the samples in (atol 1e-5 of the matrix scale), symmetric (off-diagonal tiles are stored
+    transposed; inside a diagonal tile (w x_a) x_b and (w x_b) x_a round apart, as sklearn's
+    np.dot(resp * diff.T, diff) does).  K not a multiple of the components per workgroup
+    included."""
     rng = np.random.RandomState(V + K + d)
     t = lambda a: torch.as_tensor(a, device=dev())  # noqa: E731
     x = t(rng.standard_normal((V, d)).astype(np.float32))
@@ -282,7 +284,7 @@ def test_scatter_default_and_fallback_agree(V, K, d, chunks):
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
     np.testing.assert_allclose(out[1], out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
     for o in out:
-        np.testing.assert_array_equal(o, np.swapaxes(o, 1, 2))
+        np.testing.assert_allclose(o, np.swapaxes(o, 1, 2), rtol=0, atol=1e-6 * np.abs(o).max())
 
 
 def test_community2vec_trains_at_d256():
