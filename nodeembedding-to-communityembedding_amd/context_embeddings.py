@@ -175,7 +175,7 @@ class Context2Vec(object):
                     ev[1].record(stream)
                     launch_events.append(ev)
             if ex is not None:
-                if b + 1 < n_batches and self.overlap:
+                if b + 1 < n_batches and self.overlap and getattr(ex, "overlap_safe", True):
                     ex.start()  # runs beside the next batch; finished by the next start()
                 else:
                     ex.sync()   # blocking (the last batch: replicas leave train() identical)

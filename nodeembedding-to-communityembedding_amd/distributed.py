@@ -220,6 +220,12 @@ class DeltaAllReduce(object):
     xGMI collectives are bandwidth-bound per link, so few big calls beat many small ones)."""
 
     COMBINES = ("sum", "mean", "touched_mean", "hot_mean", "pick", "hot_pick")
+    # combines whose exchange may overlap the next batch (start() now, finish() after it).  pick
+    # may not: a rank that lost a row keeps training its own copy meanwhile, and finish() then
+    # adds that progress to the winner's copy -- on a 100k-node Chung-Lu graph at lr 0.1 the
+    # held-out loss diverges (+45..+130%, scripts/replicas_cpu.py) where the blocking exchange
+    # stays within a few percent (DESIGN.md §6)
+    OVERLAP_SAFE = ("sum", "mean", "touched_mean", "hot_mean")
 
     def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum",
                  mean_rows=None, pick_rows=None, same_start=True):
@@ -382,6 +388,10 @@ class DeltaAllReduce(object):
     @property
     def busy(self):
         return bool(self.pending)
+
+    @property
+    def overlap_safe(self):
+        return self.combine in self.OVERLAP_SAFE
 
     def bytes_per_sync(self):
         return sum(t.numel() * t.element_size() for t in self.tables)

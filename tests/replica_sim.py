@@ -50,7 +50,7 @@ def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negativ
             e.prepare()         # finishes the previous exchange, snapshots this one's delta
         for e in exs:
             e.start()           # launches this exchange (overlapped: finished by the next one)
-        if overlap and not last:
+        if overlap and not last and exs[0].overlap_safe:  # (as Context2Vec.train_rows)
             continue
         for e in exs:           # blocking exchange = start / finish / settle on every rank
             e.finish()

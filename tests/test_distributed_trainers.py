@@ -42,12 +42,12 @@ def _fake_o1(node, edges, seeds, negative, table, lr, mode, hot=None, opts=None)
         node.index_add_(0, e[p], torch.full((2, node.shape[1]), 1e-3, dtype=torch.float32) * s[p])
 
 
-def _setup(V=40, d=8):
+def _setup(V=40, d=8, seed=11):
     import come_amd.training_sdg_inner as tsi
     from come_amd.model import Model
     tsi.sgns_o2 = _fake_o2
     tsi.sgns_o1 = _fake_o1
-    np.random.seed(11)
+    np.random.seed(seed)
     model = Model((np.arange(1, V + 1), np.arange(1, V + 1) % 5 + 1), size=d, table_size=1000,
                   k=1, device="cpu")
     rng = np.random.RandomState(3)
@@ -147,6 +147,55 @@ def test_trainers_distributed_world2_touched_mean(tmp_path):
     for tab in ("node", "ctx"):
         ref = reference_touched_mean(ld("base_" + tab), [ld("own_%s%d" % (tab, r))
                                                          for r in range(world)])
+        for r in range(world):
+            np.testing.assert_allclose(ld("%s%d" % (tab, r)), ref, rtol=0, atol=2e-6)
+        np.testing.assert_array_equal(ld(tab + "0"), ld(tab + "1"))
+
+
+def _worker_seeded(rank, world, port, out_dir, combine):
+    """Every rank seeds numpy differently (so Model.reset_weights draws different tables)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from come_amd.context_embeddings import Context2Vec
+    from come_amd.node_embeddings import Node2Vec
+    model, walks, edges = _setup(seed=100 + rank)
+    np.save(os.path.join(out_dir, "init%d.npy" % rank), model.node_embedding.numpy().copy())
+    Context2Vec(lr=0.1, window_size=2, negative=3, distributed=True, sync_walks=5,
+                combine=combine).train(model, paths=walks, total_nodes=walks.size, alpha=1.0)
+    Node2Vec(lr=0.1, negative=3, distributed=True, combine=combine).train(model, edges=edges,
+                                                                        iter=2)
+    np.save(os.path.join(out_dir, "node%d.npy" % rank), model.node_embedding.numpy())
+    np.save(os.path.join(out_dir, "ctx%d.npy" % rank), model.context_embedding.numpy())
+    dist.destroy_process_group()
+
+
+def test_trainers_distributed_ranks_seeded_differently(tmp_path):
+    """the exchange adds deltas to each rank's own W_sync, so replicas that start apart
+    would never meet.  The exchange takes rank 0's tables when it is built (a broadcast), so ranks
+    seeded differently still leave train() with identical replicas."""
+    world = 2
+    mp.spawn(_worker_seeded, args=(world, _free_port(), str(tmp_path), "touched_mean"),
+             nprocs=world, join=True)
+    ld = lambda n: np.load(os.path.join(str(tmp_path), n + ".npy"))  # noqa: E731
+    assert not np.array_equal(ld("init0"), ld("init1"))   # the ranks did start apart
+    np.testing.assert_array_equal(ld("node0"), ld("node1"))
+    np.testing.assert_array_equal(ld("ctx0"), ld("ctx1"))
+
+
+def test_trainers_distributed_world2_pick(tmp_path):
+    """combine='pick', one exchange: a row changed by both ranks takes rank 0's delta (the star
+    of exchange 0), a row changed by one rank its delta (distributed.reference_pick); replicas
+    identical.  pick never overlaps its exchange (DeltaAllReduce.OVERLAP_SAFE)."""
+    from come_amd.distributed import DeltaAllReduce, reference_pick
+    assert "pick" not in DeltaAllReduce.OVERLAP_SAFE
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), 1 << 17, True, "pick"),
+             nprocs=world, join=True)
+    ld = lambda n: np.load(os.path.join(str(tmp_path), n + ".npy"))  # noqa: E731
+    for tab in ("node", "ctx"):
+        ref = reference_pick(ld("base_" + tab), [ld("own_%s%d" % (tab, r)) for r in range(world)],
+                             0)
         for r in range(world):
             np.testing.assert_allclose(ld("%s%d" % (tab, r)), ref, rtol=0, atol=2e-6)
         np.testing.assert_array_equal(ld(tab + "0"), ld(tab + "1"))

@@ -293,11 +293,12 @@ def test_hot_rows_bitmap_matches_table_counts():
             np.testing.assert_array_equal(got, cnt >= mc)
 
 
-def karate_flow(seed, gpu):
+def karate_flow(seed, gpu, distributed=False):
     """adsc_Karate.py:104-137 (+ the final fit of :148) on the shipped Karate graph and the walks
     the reference's own walker produced (tests/golden/karate.npz): pre-train O1 + O2, then one
     loop of O1, O2, GMM fit (sklearn, unseeded: global numpy RNG), community step x5, GMM fit.
-    gpu=True: come_amd trainers in Hogwild mode; gpu=False: the oracle (sequential C SGNS,
+    gpu=True: come_amd trainers in Hogwild mode (distributed=True: the multi-GPU trainers over the
+    initialised process group, their default exchange); gpu=False: the oracle (sequential C SGNS,
     numpy community step).  Returns argmax of the responsibilities per node row."""
     from sklearn.mixture import GaussianMixture
     z = np.load(os.path.join(GOLDEN, "karate.npz"))
@@ -312,8 +313,8 @@ def karate_flow(seed, gpu):
         from come_amd.node_embeddings import Node2Vec
         model = Model((z["degree_ids"], z["degree_counts"]), size=size, table_size=T, k=2,
                       device=DEV)
-        nl = Node2Vec(workers=1, negative=neg, lr=lr)
-        cl = Context2Vec(window_size=ws, workers=1, negative=neg, lr=lr)
+        nl = Node2Vec(workers=1, negative=neg, lr=lr, distributed=distributed)
+        cl = Context2Vec(window_size=ws, workers=1, negative=neg, lr=lr, distributed=distributed)
         cm = Community2Vec(model, reg_covar=1e-5, lr=lr, gmm_backend="sklearn")
         for _ in range(2):
             nl.train(model, edges=z["edges"], iter=1, chunksize=20)
@@ -356,6 +357,45 @@ def test_karate_nmi_hogwild_within_reference_range():
         np.round(gpu, 3), np.mean(gpu), np.round(cpu, 3), np.mean(cpu)))
     assert 0.48 <= np.mean(gpu) <= 0.73, gpu
     assert abs(np.mean(gpu) - np.mean(cpu)) <= 0.1, (gpu, cpu)
+
+
+def _karate_ranks_worker(rank, world, port, out_dir, seeds):
+    """One rank of the multi-GPU Karate flow: `world` processes on cuda:0 over gloo (RCCL needs one
+    GPU per rank; the trainers' exchange arithmetic is the same)."""
+    import torch.distributed as dist
+    from sklearn.metrics import normalized_mutual_info_score
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = np.load(os.path.join(GOLDEN, "karate.npz"))
+    labels = z["labels"][np.argsort(z["labels"][:, 0]), 1]
+    nmi = [normalized_mutual_info_score(labels, karate_flow(s, True, distributed=True))
+           for s in seeds]
+    np.save(os.path.join(out_dir, "nmi%d.npy" % rank), np.array(nmi))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_karate_nmi_multi_rank_within_reference_range(tmp_path, world):
+    """The reference's own quality check (adsc_Karate.py:104-148: NMI of the community assignment
+    vs karate_zachary.labels) under N-replica training: `world` ranks (processes on one GPU, gloo)
+    run the Karate flow with Context2Vec / Node2Vec(distributed=True) and the default exchange;
+    over 10 seeds the mean NMI lies in the reference's seed range 0.48-0.73 and the
+    replicas agree (every rank computes the same assignments)."""
+    import socket
+    import torch.multiprocessing as mp
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    seeds = list(range(10))
+    mp.spawn(_karate_ranks_worker, args=(world, port, str(tmp_path), seeds), nprocs=world,
+             join=True)
+    nmi = [np.load(str(tmp_path / ("nmi%d.npy" % r))) for r in range(world)]
+    for r in range(1, world):
+        np.testing.assert_array_equal(nmi[r], nmi[0])
+    print("Karate NMI, %d ranks: %s mean %.3f" % (world, np.round(nmi[0], 3), nmi[0].mean()))
+    assert 0.48 <= nmi[0].mean() <= 0.73, nmi[0]
 
 
 # ---- configs[4]/C5 (d = 256, n = 10) -----------------------------------------------------------
@@ -515,3 +555,50 @@ def test_o2_eight_ranks_default_period_over_4m_walks():
     print("C3 4M walks, 8 ranks x %d walks per exchange: held-out loss %.5f vs seq %.5f "
           "(rel %+.5f)" % (DEFAULT_SYNC_WALKS, loss, fx["seq_loss"], rel))
     assert np.isfinite(loss) and -0.25 < rel < 0.01, (loss, fx["seq_loss"])
+
+
+@pytest.fixture(scope="module")
+def c2_reference_order(c2_shape):
+    """C2 in the reference's own edge order (np.array(G.edges()), node_embeddings.py:39) with 4
+    passes' worth of per-edge seeds (Node2Vec.train(iter=4)) and the sequential oracle's held-out
+    losses after them (one core, ~1 s per pass)."""
+    g, table, train, held, node0, _ = c2_shape
+    train = train[np.lexsort((train[:, 1], train[:, 0]))]
+    srng = np.random.RandomState(33)
+    seeds = [srng.randint(0, 2 ** 48, len(train), dtype=np.int64).astype(np.uint64)
+             for _ in range(4)]
+    neg = table[np.random.RandomState(32).randint(0, len(table), (len(held), 5))].astype(np.int64)
+
+    def losses(x):
+        ref = float(-log_sigmoid(np.einsum("pd,pd->p", x[held[:, 1]].astype(np.float64),
+                                           x[held[:, 0]].astype(np.float64))).sum())
+        return ref, sgns_loss(x, x, held[:, 0], held[:, 1], neg)
+    seq = node0.copy()
+    for sd in seeds:
+        orc.sgns_o1_hogwild(seq, train, sd, 5, table, 0.1, threads=1)
+    tab = dev(table)
+    hot = tsi.hot_rows(tab, g.V, int(tsi.DEFAULT_HOT_P * len(table)))
+    return g, train, node0, seeds, tsi.pack_table(tab), hot, losses, losses(seq)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_o1_multi_rank_exchange_tier_c(c2_reference_order, world):
+    """Multi-GPU O1 (Node2Vec(distributed=True), node_embeddings.py:35-106): `world` ranks
+    simulated on one GPU (tests/replica_sim.train_replicas_o1: each rank its contiguous shard of
+    every pass, the product's launch, one blocking exchange per pass with the trainers' default
+    combine, RCCL replaced by a sum over the replicas), 4 passes = 4 exchanges, in the reference's
+    G.edges() order: both held-out losses (the reference's :26-31 and SGNS) within 1% of the
+    sequential oracle's, either side (SURVEY.md §8c tier C)."""
+    from come_amd.node_embeddings import Node2Vec
+    from replica_sim import train_replicas_o1
+    g, train, node0, seeds, packed, hot, losses, l_seq = c2_reference_order
+    st = {}
+    x = train_replicas_o1(node0, train, seeds, world, None, 5, packed, hot, 0.1,
+                          combine=Node2Vec().combine, stats=st)
+    l = losses(x.cpu().numpy())
+    rel = [(a - b) / b for a, b in zip(l, l_seq)]
+    print("O1 %d ranks, %d exchanges: held-out (reference / SGNS) %.1f / %.5f vs seq %.1f / %.5f "
+          "(rel %+.4f / %+.4f)" % ((world, st["exchanges"]) + l + l_seq + tuple(rel)))
+    assert st["exchanges"] == 4
+    assert max(abs(r) for r in rel) < 0.01, (l, l_seq)
+
