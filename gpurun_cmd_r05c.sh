@@ -1,7 +1,4 @@
-# Evidence at HEAD: rocprofv3 kernel stats + HBM traffic of the default bench launch (C3), kernel
-# stats of the C2 and C4 rows, then the default bench line.
+# Full GPU suite + smoke at HEAD.
 bash scripts/steps.sh r05c \
- "prof_c3|900|TAG=r05c STEPS=5 bash scripts/profile.sh && python scripts/summarize_profile.py gpurun_out/prof_r05c r05c" \
- "prof_c2|300|cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/prof_r05c_c2 -o run -- python3 \$GRAFT_REPO_ROOT/bench_aux.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline" \
- "prof_c4|300|cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/prof_r05c_c4 -o run -- python3 \$GRAFT_REPO_ROOT/bench_aux.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline" \
- "bench|600|python bench.py"
+ "pytest|1000|python -u -m pytest tests -m gpu -q -rs --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'"

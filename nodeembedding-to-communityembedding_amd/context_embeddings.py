@@ -26,9 +26,12 @@ deltas ("sum", the first-order merge) diverges at lr 0.1: within any practical p
 trajectory saturates on every rank (hub rows take thousands of updates per rank per period), so
 N saturated displacements add up to N times the step (held-out loss 6-100 vs the sequential
 oracle's 2.56 at 2-8 ranks).  Averaging is stable and trains to a LOWER held-out
-loss than the sequential oracle (less SGD noise); it is not the reference's trajectory, which no
-periodic exchange reproduces at this learning rate.  train() ends with a blocking exchange: every
-replica then holds the same tables.
+loss than the sequential oracle (less SGD noise, -12..-19%); it is not the reference's trajectory,
+which no periodic exchange reproduces at this learning rate: ``combine="pick"`` (each row takes one
+rank's delta, blocking exchanges) keeps the reference's noise level but only 1/N of the shared
+rows' progress (+0.8% at 2 ranks, +10% at 8).  Distributed training is therefore NOT a parity mode
+(INTEGRATION.md).  The exchange starts every replica from rank 0's tables; train() ends with a
+blocking exchange, so every replica then holds the same tables.
 """
 import logging as log
 import time

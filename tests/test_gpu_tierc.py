@@ -590,11 +590,11 @@ def c2_reference_order(c2_shape):
     return g, train, node0, seeds, tsi.pack_table(tab), hot, losses, losses(seq)
 
 
-# |held-out loss / sequential oracle's - 1| of Node2Vec(distributed=True)'s exchange (touched_mean,
-# one per pass) after 4 passes, measured (profiles/r05_tierc_replicas_c2_4pass.json): reference
-# loss / SGNS loss -1.4 / -2.0% at 2 ranks, +0.5 / -0.5% at 4, +3.1 / +1.9% at 8 -- tier C (1%) at 4
-# ranks only; the bands guard the measured values.
-O1_MULTI_RANK_BAND = {2: 0.03, 4: 0.01, 8: 0.045}
+# |held-out loss / sequential oracle's - 1| allowed for Node2Vec(distributed=True) after 4 passes
+# (SURVEY.md §8c tier C).  The round-4 touched_mean exchange measured -1.4 / -2.0% (reference /
+# SGNS loss) at 2 ranks, +0.5 / -0.5% at 4, +3.1 / +1.9% at 8 (profiles/r05_tierc_replicas_c2_4pass
+# .json); the default is now owner-computes (node_embeddings.py).
+O1_MULTI_RANK_BAND = {2: 0.01, 4: 0.01, 8: 0.01}
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
