@@ -35,8 +35,7 @@ extern "C" {
 
 /* ABI 3 (this header): the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B
  * kernels) was removed, "community_async" accepts 1 / 2, "gmm_cov_async" 1 / 3 and "gmm_resp16"
- * 0 / 2 (other values: COME_E_INVALID at the call); the options "o1_own_lo" / "o1_own_hi" and
- * come_source_sha256 were added.
+ * 0 / 2 (other values: COME_E_INVALID at the call); come_source_sha256 was added.
  * ABI 2: come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
  * options "o2_plain_writeback" and "o2_pair_atomics" (ABI 1, ring-kernel Hogwild) were removed and
@@ -282,11 +281,6 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       grid (the edges in flight spread over the whole list: tier C holds in
  *                       the reference's G.edges() order, +0.23% vs 1.6% for 0); 0 = one
  *                       wavefront per edge (k_sgns_o1).  Sequential mode: one chunk, in order
- *   o1_own_lo / o1_own_hi  O1 run kernel: only the pairs whose INPUT row lies in [lo, hi) run
- *                       (pair 1 of edge (u, v) updates u, pair 2 updates v, pyx:444-448), the
- *                       other rows are read-only; the multi-GPU owner-computes partition
- *                       (Node2Vec(distributed=True, combine="owner")).  0 / 0 = every row; with
- *                       o1_chunk = 0 a range is COME_E_INVALID
  *   o2_update_count     (per call, come_sgns_o2_ex only) device uint64: += the number of target
  *                       row updates the launch applied (positive + negatives that passed the
  *                       +-6 skip, pyx:141-147) -- what the data-dependent part of the O2 HBM
@@ -308,8 +302,6 @@ typedef struct come_launch_opts {
     int o2_atomic_writeback;
     int gmm_resp16;
     int o1_chunk;
-    int o1_own_lo;
-    int o1_own_hi;
     uint64_t *o2_update_count;
 } come_launch_opts;
 

@@ -35,7 +35,7 @@ OPTION_FIELDS = ("o2_kernel", "o2_blocks_per_cu", "o2_waves_per_block",
                  "o2_static", "rows_per_wave", "o1_rows_per_wave",
                  "max_waves", "o1_blocks_per_cu", "resident_cap", "community_async",
                  "gmm_cov_async", "walk_staged", "o2_fresh_loads", "o2_atomic_writeback",
-                 "gmm_resp16", "o1_chunk", "o1_own_lo", "o1_own_hi")
+                 "gmm_resp16", "o1_chunk")
 
 
 class LaunchOpts(ctypes.Structure):

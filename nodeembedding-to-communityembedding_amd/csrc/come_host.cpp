@@ -161,8 +161,7 @@ extern "C" int come_set_option(const char *name, int value) {
                   COME_OPT(gmm_cov_async),    COME_OPT(walk_staged),
                   COME_OPT(o2_fresh_loads),   COME_OPT(o2_atomic_writeback),
                   COME_OPT(gmm_resp16),
-                  COME_OPT(o1_chunk),         COME_OPT(o1_own_lo),
-                  COME_OPT(o1_own_hi)};
+                  COME_OPT(o1_chunk)};
 #undef COME_OPT
     for (const auto &f : fields)
         if (!strcmp(f.k, name)) {

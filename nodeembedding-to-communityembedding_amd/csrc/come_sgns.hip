@@ -238,17 +238,8 @@ extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edg
         const int64_t waves = mode == COME_MODE_HOGWILD ? 4 * blocks : 1;
         chunk = (E + waves - 1) / waves;
     }
-    // owner range (o1_own_lo / o1_own_hi, multi-GPU owner-computes): only pairs whose input row
-    // lies in it run; 0 / 0 = every row
-    const bool owned = o.o1_own_hi > 0;
-    if (owned && (o.o1_own_lo < 0 || o.o1_own_lo >= o.o1_own_hi || o.o1_own_hi > V))
-        return set_error(COME_E_INVALID, "o1_own range [%d, %d) must lie in [0, V)", o.o1_own_lo,
-                         o.o1_own_hi);
-    if (owned && chunk == 0)
-        return set_error(COME_E_INVALID, "o1_own ranges need the run kernel (o1_chunk != 0)");
     O1Args a{node,           edges, seeds, table, V, E, d, negative, lr, make_fastmod(T), packed,
-             mode == COME_MODE_HOGWILD ? hot_rows : nullptr, chunk > 0 ? chunk : 1,
-             owned ? (int64_t)o.o1_own_lo : 0, owned ? (int64_t)o.o1_own_hi : V};
+             mode == COME_MODE_HOGWILD ? hot_rows : nullptr, chunk > 0 ? chunk : 1};
     int full = 0;
     const KernelSet &ks = kernel_set(d, &full);
     if (chunk > 0)  // one wavefront per chunk of consecutive edges, the input row held

@@ -1154,7 +1154,6 @@ struct O1Args {
     int packed;
     const uint32_t *hot;  // HOG, optional: contended rows (come_hot_rows), updated atomically
     int64_t chunk;        // k_sgns_o1_runs: consecutive edges per wavefront unit
-    int64_t own_lo, own_hi;  // k_sgns_o1_runs: only the pairs whose input row is in [lo, hi) run
 };
 
 template <int VEC, bool FULL, int MAXN>
@@ -1312,16 +1311,7 @@ __global__ void __launch_bounds__(256)
             const int u = uniform(a.edges[2 * e]);
             const int v = uniform(a.edges[2 * e + 1]);
             if (u < 0 || u >= a.V || v < 0 || v >= a.V) continue;  // reference: undefined
-            // owner range (multi-GPU owner-computes): pair 1 updates u, pair 2 updates v; a pair
-            // whose input row another rank owns is that rank's (wave-uniform)
-            const bool run1 = u >= a.own_lo && u < a.own_hi;
-            const bool run2 = v >= a.own_lo && v < a.own_hi;
-            if (!run1 && !run2) continue;
-            if (!run1) {  // pair 2 only: u is a read-only positive (this rank's copy)
-                flush();
-                cu = -1;
-                hu.load(a.node + (int64_t)u * d, lane, d);
-            } else if (u != cu) {
+            if (u != cu) {
                 flush();
                 cu = u;
                 hot_cu = is_hot(a, u);
@@ -1344,8 +1334,8 @@ __global__ void __launch_bounds__(256)
                 if (k <= n) {
                     t1[k] = (int)readlane_u32(db.target, k - 1);
                     t2[k] = (int)readlane_u32(db.target, n + k - 1);
-                    v1[k] = run1 && t1[k] != v && t1[k] >= 0 && t1[k] < a.V;
-                    v2[k] = run2 && t2[k] != u && t2[k] >= 0 && t2[k] < a.V;
+                    v1[k] = t1[k] != v && t1[k] >= 0 && t1[k] < a.V;
+                    v2[k] = t2[k] != u && t2[k] >= 0 && t2[k] < a.V;
                 } else {
                     t1[k] = t2[k] = -1;
                     v1[k] = v2[k] = false;
@@ -1365,7 +1355,7 @@ __global__ void __launch_bounds__(256)
             }
             r1[0] = v != u ? in2 : hu;  // pair 1's positive node[v] (pre-update)
             // pair 1: input = the held u
-            if (run1) {
+            {
                 float part[MAXN + 1];
 #pragma unroll
                 for (int k = 0; k <= MAXN; ++k) part[k] = v1[k] ? lane_partial(hu, r1[k]) : 0.0f;
@@ -1395,7 +1385,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
             for (int k = 1; k <= MAXN; ++k)
                 if (v2[k] && t2[k] == v) r2[k] = in2;
-            if (run2) {
+            {
                 float part[MAXN + 1];
 #pragma unroll
                 for (int k = 0; k <= MAXN; ++k) part[k] = v2[k] ? lane_partial(in2, r2[k]) : 0.0f;

@@ -8,18 +8,11 @@ trains the pairs (edge[0] -> edge[1]) then (edge[1] -> edge[0]) on node_embeddin
 (Hogwild across edges) or, with ``deterministic=True``, one wavefront in edge order (== the
 reference with workers=1).  ``loss`` reproduces :26-31 (-sum log sigma(u.v) over the edges).
 
-Multi-GPU (``distributed=True``): every rank is handed the same edge list and
-draws every edge's seed per pass (the global numpy RNG advances as in one process).
-  * ``combine="owner"`` (default): owner-computes.  O1 writes only a pair's INPUT row (pair 1 of
-    edge (u, v) updates u, pair 2 updates v, pyx:444-448), so rank r runs exactly the pairs whose
-    input row lies in its row block shard_range(V, r, N) -- every update is applied once, by the
-    row's owner, and no two ranks write a row -- reading the other rows from its replica; after
-    each pass the row blocks are all-gathered (distributed.all_gather_rows over RCCL).  Two
-    launches per pass: the edges whose first endpoint the rank owns (both pairs where owned, in
-    edge order) and the edges whose second endpoint only it owns (pair 2).
-  * any DeltaAllReduce combine (e.g. "touched_mean"): each rank trains its contiguous shard of
-    each pass and exchanges its progress after every ``sync_edges`` of its edges and at the end
-    of each pass (blocking: an O1 pass is ~1 ms at C2).
+Multi-GPU (``distributed=True``): every rank is handed the same edge list, draws
+every edge's seed per pass (the global numpy RNG advances as in one process), trains its
+contiguous shard of each pass and exchanges its node_embedding progress with the other ranks
+after every ``sync_edges`` of its edges and at the end of each pass (DeltaAllReduce over RCCL,
+combine rule touched_mean as Context2Vec's; blocking: an O1 pass is ~1 ms at C2).
 """
 import logging as log
 import time
@@ -31,7 +24,7 @@ from . import training_sdg_inner as tsi
 
 class Node2Vec(object):
     def __init__(self, lr=0.2, workers=1, negative=0, deterministic=False, distributed=False,
-                 sync_edges=None, group=None, combine="owner"):
+                 sync_edges=None, group=None, combine="touched_mean"):
         self.workers = workers
         self.lr = float(lr)
         self.negative = negative
@@ -57,41 +50,6 @@ class Node2Vec(object):
             return self._exchanges[key]
         ex.reset()
         return ex
-
-    def _train_owner(self, model, edges, rows, ed, mode, hot, rank, world, iters, start):
-        """The owner-computes passes (see the module docstring)."""
-        import torch
-        from .distributed import all_gather_rows, shard_range
-        V = model.node_embedding.shape[0]
-        lo, hi = shard_range(V, rank, world)
-        opts = {"o1_own_lo": lo, "o1_own_hi": hi}
-        dev = model.node_embedding.device
-        from .distributed import TorchComm
-        TorchComm(self.group).broadcast(model.node_embedding, 0)  # replicas start from rank 0's
-        pairs = 0
-        for it in range(int(iters)):
-            if it > 0 and model.down_sampling:  # every pass draws its own sample (:47)
-                rows = self._edge_rows(model, edges)
-                ed = torch.from_numpy(rows).to(dev)
-            seeds = tsi.draw_seeds(rows.shape[0])
-            sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
-            u, v = ed[:, 0], ed[:, 1]
-            own_u = (u >= lo) & (u < hi)
-            own_v = (v >= lo) & (v < hi) & (u >= 0)
-            for sel in (own_u, own_v & ~own_u):
-                idx = torch.nonzero(sel).view(-1)
-                if idx.numel():
-                    tsi.sgns_o1(model.node_embedding, ed[idx].contiguous(), sd[idx].contiguous(),
-                                self.negative, model.negative_table(), self.lr, mode, hot=hot,
-                                opts=opts)
-            pairs += int(own_u.sum()) + int((own_v & (u >= 0)).sum())
-            all_gather_rows(model.node_embedding, self.group)
-        if model.node_embedding.is_cuda:
-            torch.cuda.synchronize(dev)
-        elapsed = time.time() - start
-        log.info("O1 training (owner-computes, rank %d of %d): %i pair updates took %.2fs", rank,
-                 world, pairs, elapsed)
-        return pairs
 
     def _edge_rows(self, model, edges):
         """Edges -> [E, 2] int32 rows as prepare_sentences would pass them to train_o1: OOV
@@ -129,8 +87,6 @@ class Node2Vec(object):
         hot = None if self.deterministic else model.hot_rows()
         from .distributed import shard_range, world_of
         rank, world = world_of(self.group) if self.distributed else (0, 1)
-        if world > 1 and self.combine == "owner":
-            return self._train_owner(model, edges, rows, ed, mode, hot, rank, world, iter, start)
         ex = self.exchange(model) if world > 1 else None
         pairs = 0
         for it in range(int(iter)):

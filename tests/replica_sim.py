@@ -64,20 +64,15 @@ def train_replicas(node0, ctx0, walks, seeds, world, sync_walks, window, negativ
 
 
 def train_replicas_o1(node0, edges, seeds_per_pass, world, sync_edges, negative, table, hot, lr,
-                      device="cuda", combine="owner", stats=None):
-    """N ranks of Node2Vec(distributed=True).train (node_embeddings.py) in one process.
-    combine "owner" (the trainer's default): every pass each rank runs the pairs whose input row
-    lies in its row block (two launches: the edges whose first endpoint it owns, then those whose
-    second endpoint only it owns, launch option o1_own_lo / o1_own_hi), then the row blocks are
-    all-gathered (copied between the replicas).  Any DeltaAllReduce combine: each rank trains its
-    contiguous shard of the edge list in launches of ``sync_edges`` edges (None = the whole
-    shard), each followed by the trainer's blocking exchange (RCCL replaced by LocalReplicas).
+                      device="cuda", combine="pick", stats=None):
+    """N ranks of Node2Vec(distributed=True).train (node_embeddings.py) in one process: every pass
+    each rank trains its contiguous shard of the edge list (distributed.shard_range) in launches
+    of ``sync_edges`` edges (None = the whole shard), each followed by the trainer's blocking
+    exchange of node_embedding (DeltaAllReduce, RCCL replaced by LocalReplicas).
     seeds_per_pass: list of uint64 [E] arrays, one per pass (every rank draws every edge's seed).
     Returns the node table (a CUDA tensor; all replicas equal)."""
     from come_amd.distributed import shard_range
     dev = torch.device(device)
-    if combine == "owner":
-        return _owner_o1(node0, edges, seeds_per_pass, world, negative, table, hot, lr, dev, stats)
     group = LocalReplicas(world)
     reps, exs = [], []
     for r in range(world):
@@ -109,35 +104,4 @@ def train_replicas_o1(node0, edges, seeds_per_pass, world, sync_edges, negative,
         assert torch.equal(reps[r], reps[0])
     if stats is not None:
         stats["exchanges"] = exs[0].exchanges
-    return reps[0]
-
-
-def _owner_o1(node0, edges, seeds_per_pass, world, negative, table, hot, lr, dev, stats):
-    from come_amd.distributed import shard_range
-    reps = [torch.from_numpy(np.ascontiguousarray(node0)).to(dev) for _ in range(world)]
-    ed = torch.from_numpy(np.ascontiguousarray(edges, np.int32)).to(dev)
-    V = reps[0].shape[0]
-    u, v = ed[:, 0], ed[:, 1]
-    for seeds in seeds_per_pass:
-        sd = torch.from_numpy(np.ascontiguousarray(seeds, np.uint64).view(np.int64)).to(dev)
-        for r in range(world):
-            lo, hi = shard_range(V, r, world)
-            own_u = (u >= lo) & (u < hi)
-            own_v = (v >= lo) & (v < hi) & (u >= 0)
-            for sel in (own_u, own_v & ~own_u):
-                idx = torch.nonzero(sel).view(-1)
-                if idx.numel():
-                    tsi.sgns_o1(reps[r], ed[idx].contiguous(), sd[idx].contiguous(), negative,
-                                table, lr, tsi.MODE_HOGWILD, hot=hot,
-                                opts={"o1_own_lo": lo, "o1_own_hi": hi})
-        for r in range(world):          # all-gather of the row blocks
-            lo, hi = shard_range(V, r, world)
-            for q in range(world):
-                if q != r:
-                    reps[q][lo:hi].copy_(reps[r][lo:hi])
-    torch.cuda.synchronize(dev)
-    for r in range(1, world):
-        assert torch.equal(reps[r], reps[0])
-    if stats is not None:
-        stats["exchanges"] = len(seeds_per_pass)
     return reps[0]
