@@ -29,6 +29,17 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #else
 #define COME_PRIO(x) ((void)0)
 #endif
+// A/B hooks of k_gmm_cov16 (build_ab.sh only; results are garbage for DIAG != 0):
+// COME_COV_DIAG 1 = staging re-stages the first 3 blocks' registers (no global loads after the
+// prologue), 2 = MFMA wavefronts consume buffer 0 without barriers (the MFMA stream alone), 3 =
+// every load reads the chunk's first block (the same instructions, cache-resident data).
+// COME_RESP_DIAG (k_gmm_resp16t) 1 = no copies after component 0, 2 = and no barriers.
+#ifndef COME_COV_DIAG
+#define COME_COV_DIAG 0
+#endif
+#ifndef COME_RESP_DIAG
+#define COME_RESP_DIAG 0
+#endif
 constexpr int kThreads = 256;
 
 // out[r][c] = sum_j A[r][j] * B(c, j) for the tile, where B(c, j) = Bm[c*d + j] (TRANS=false,
@@ -999,10 +1010,12 @@ template <int D>
 struct Resp16T {
     static constexpr int NQ = D / 16;
     static constexpr int TRI = 16 * 16 * NQ * (NQ + 1) / 2;  // floats of the packed blocks
-    static constexpr int MP = TRI;                            // mu_k P_k (256 reserved)
-    static constexpr int PAR = TRI + 256;                     // lower flag, log_norm (64 reserved)
-    static constexpr int BUF = TRI + 256 + 64;                // floats per buffer
-    static constexpr int LDS = 2 * BUF;
+    static constexpr int MP = 0;                              // in a slot: mu_k P_k (256 reserved)
+    static constexpr int PAR = 256;                           // lower flag, log_norm (64 reserved)
+    static constexpr int SLOT = 256 + 64;                     // floats per parameter slot
+    static constexpr int LDS = 2 * (TRI + SLOT);              // two buffers
+    __device__ static float *blocks(float *sm, int k) { return sm + (k & 1) * TRI; }
+    __device__ static float *slot(float *sm, int k) { return sm + 2 * TRI + (k & 1) * SLOT; }
     static constexpr int PIECES = TRI / 256;
     static_assert(TRI % 256 == 0, "whole 1 KiB pieces");
     // offset of quad q's first row block: 16 floats x sum_{q' < q} (D - 16 q') rows
@@ -1036,11 +1049,11 @@ struct R16tShape {
     static constexpr int WPE = 4;                // waves per SIMD the registers must allow
 };
 
-// component k's packed blocks, mu_k P_k, lower flag and log_norm into `buf` (NW wavefronts share
-// the 1 KiB copies)
+// component k's packed blocks into `buf`, its mu_k P_k, lower flag and log_norm into `par` (NW
+// wavefronts share the 1 KiB copies)
 template <int D>
-__device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf, int wid,
-                                           int lane) {
+__device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf, float *par,
+                                           int wid, int lane) {
     using T = Resp16T<D>;
     constexpr int NW = R16tShape::NW;
     const float *src = a.prec_t + (int64_t)k * T::TRI;  // the packed blocks in this body
@@ -1052,11 +1065,11 @@ __device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf,
     }
     if (wid == 0) {
         const int s = lane * 4 < D ? lane * 4 : D - 4;
-        __builtin_amdgcn_global_load_lds(a.mu_prec + (int64_t)k * D + s, buf + T::MP, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(a.mu_prec + (int64_t)k * D + s, par + T::MP, 16, 0, 0);
     } else if (wid == 1) {
         const float *p = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
                                    : a.log_norm + k;
-        __builtin_amdgcn_global_load_lds(p, buf + T::PAR, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(p, par + T::PAR, 4, 0, 0);
     }
 }
 
@@ -1102,6 +1115,8 @@ __device__ __forceinline__ void r16t_blocks(
     for (int n = 0; n < NB; ++n) {
         if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
         const int q = TB.q[n], ct = TB.ct[n];
+        // quad 0's blocks (n < NQ) start acc[ct] from zero: the accumulator is born here
+        if (q == 0) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[n % 3][t], xb[q][t], acc[ct], 0, 0, 0);
@@ -1110,29 +1125,22 @@ __device__ __forceinline__ void r16t_blocks(
     COME_PRIO(0);
 }
 
-// log N(x_row; mu_k, P_k) of the lane's row for the component in `buf`
+// the epilogue of one component: sq += |acc[ct] - (mu_k P_k)[ct]|^2 over the column tiles ct in
+// order, then log N(x_row; mu_k, P_k) = log_norm_k - sq / 2 summed over the lane groups
 template <int D>
-__device__ __forceinline__ float r16t_lp(const __attribute__((ext_vector_type(4))) float (&xb)[D / 16],
-                                         const float *buf, int abase, int kg) {
-    using T = Resp16T<D>;
-    constexpr int NQ = T::NQ;
+__device__ __forceinline__ void r16t_sq(const __attribute__((ext_vector_type(4))) float &acc,
+                                        const float *par, int ct, int kg, float &sq) {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    const float lnk = buf[T::PAR + 1];
-    f32x4 acc[NQ];
+    const f32x4 mp = *reinterpret_cast<const f32x4 *>(par + Resp16T<D>::MP + ct * 16 + 4 * kg);
 #pragma unroll
-    for (int ct = 0; ct < NQ; ++ct) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    r16t_blocks<D>(xb, buf, abase, acc);
-    float sq = 0.0f;
-#pragma unroll
-    for (int ct = 0; ct < NQ; ++ct) {
-        const f32x4 mp = *reinterpret_cast<const f32x4 *>(buf + T::MP + ct * 16 + 4 * kg);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float y = acc[ct][e] - mp[e];
-            sq = __builtin_fmaf(y, y, sq);
-        }
+    for (int e = 0; e < 4; ++e) {
+        const float y = acc[e] - mp[e];
+        sq = __builtin_fmaf(y, y, sq);
     }
-    return lnk - 0.5f * reduce_stage<5>(reduce_stage<4>(sq));
+}
+template <int D>
+__device__ __forceinline__ float r16t_lp_of(float sq, const float *par) {
+    return par[Resp16T<D>::PAR + 1] - 0.5f * reduce_stage<5>(reduce_stage<4>(sq));
 }
 
 // online log-sum-exp step
@@ -1168,7 +1176,7 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
             if (row < a.V) xb[q] = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * q + 4 * kg);
         }
     }
-    r16t_stage<D>(a, 0, sm, wid, lane);
+    r16t_stage<D>(a, 0, T::blocks(sm, 0), T::slot(sm, 0), wid, lane);
     // the lane's A operands of block (q, ct): row ct*16 + j16 of quad q's row block
     const int abase = j16 * 16 + 4 * (kg ^ ((j16 >> 1) & 2));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1177,17 +1185,25 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
     const bool owner = kg == 0 && my_row < a.V;
     float run_max = -INFINITY, run_sum = 0.0f, lp_prev = 0.0f;
     for (int k = 0; k < a.K; ++k) {
-        const float *buf = sm + (k & 1) * T::BUF;
-        if (k + 1 < a.K) r16t_stage<D>(a, k + 1, sm + ((k + 1) & 1) * T::BUF, wid, lane);
+        if (k + 1 < a.K && !COME_RESP_DIAG)
+            r16t_stage<D>(a, k + 1, T::blocks(sm, k + 1), T::slot(sm, k + 1), wid, lane);
         // component k - 1's log-probability is stored one component late: a store counts on the
         // vector-memory counter like the staging copies, so storing it right before the barrier's
         // vmcnt(0) made every wavefront wait out the store's round trip once per component
         if (k > 0 && owner) a.resp[my_row * a.K + k - 1] = lp_prev;
-        const float lp = r16t_lp<D>(xb, buf, abase, kg);
+        const float *par = T::slot(sm, k);
+        f32x4 acc[NQ];
+        r16t_blocks<D>(xb, T::blocks(sm, k), abase, acc);
+        float sq = 0.0f;
+#pragma unroll
+        for (int ct = 0; ct < NQ; ++ct) r16t_sq<D>(acc[ct], par, ct, kg, sq);
+        const float lp = r16t_lp_of<D>(sq, par);
         lse_push(lp, run_max, run_sum);
         lp_prev = lp;
+#if COME_RESP_DIAG != 2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
+#endif
     }
     if (owner) {
         float *lp = a.resp + my_row * a.K;
@@ -1598,10 +1614,18 @@ __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, 
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr Cov16Tiles<D> TT{};
     const int j16 = lane & 15, kg = lane >> 4;
+#if COME_COV_DIAG == 2
+    __syncthreads();
+#endif
     for (int j = 0; j < nb; ++j) {
+#if COME_COV_DIAG == 2
+        asm volatile("" ::: "memory");  // keep the LDS reads in the loop
+        const float *buf = img;
+#else
         __syncthreads();  // barrier j: block j staged
-        COME_PRIO(1);
         const float *buf = img + (j % C::NBUF) * C::BUF;
+#endif
+        COME_PRIO(1);
         const float *im = buf + tk * C::IMG;
 #pragma unroll
         for (int g = 0; g < C::RB / 16; ++g) {
@@ -1635,7 +1659,7 @@ __device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, 
 // the MFMA part of wavefront part P (compile-time tile tables): consume, then store the tiles
 template <int D, int P>
 __device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, int nb, int tk,
-                                           int nk, int k0, int lane) {
+                                           int nk, int k0, int64_t chunk, int lane) {
     using C = Cov16<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     f32x4 acc[C::NTW];
@@ -1645,7 +1669,7 @@ __device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, i
     if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
     constexpr Cov16Tiles<D> TT{};
     const int j16 = lane & 15, kg = lane >> 4;
-    float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
+    float *out = a.out + (chunk * a.K + k0 + tk) * D * D;
 #pragma unroll
     for (int n = 0; n < C::NTW; ++n) {
         const int rt = TT.rows[P][TT.slot[P][n]], ct = TT.ct[P][n];
@@ -1659,21 +1683,162 @@ __device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, i
     }
 }
 
+// k_gmm_cov16's staging wavefronts (256 threads, thread st): block blk of the chunk [c0, c1) goes
+// global -> VGPR register set u (three sets: loads run 3 blocks ahead of the stage that consumes
+// them, an HBM / MALL round trip under load exceeding one block period) -> centred, transposed
+// LDS image per component (stage), with the weights beside it.
+// d = 128: 16-byte loads.  Thread st < RB D / 16 owns feature quad fq = st / 8 (features 4 fq ..
+// 4 fq + 3) of samples 4 sg .. 4 sg + 3, sg = st % 8: one dwordx4 per sample, 8 lanes reading one
+// 128-B line; each feature's 4 samples become one b128 granule (8 consecutive lanes write the 8
+// granules of one image row: conflict-free).  Thread st < CPW RB carries the weight of sample
+// st % RB for component st / RB.  (vs one dword per column and sample: 7.27 vs 7.40 ms at C4,
+// bit-identical, profiles/r05_ab_gmm_diag.txt; the d = 64 form below needs too many registers this
+// way: 16 means per thread.)
+template <int D>
+struct Cov16StageX4 {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    static constexpr int RB = C::RB, CPW = C::CPW, NX = RB * D / 16;
+    static_assert(RB == 32 && NX <= 256 && CPW * RB <= 256, "x4 staging layout");
+    const CovArgs &a;
+    const int sg, fq, wk, ws, k0, nk;
+    const bool xl, wlane;
+    const int64_t c0, c1;
+    float mu[CPW][4];
+    f32x4 xv[3][4];
+    float wl[3];
+    __device__ __forceinline__ Cov16StageX4(const CovArgs &a_, int st, int k0_, int nk_, int64_t c0_,
+                                            int64_t c1_)
+        : a(a_), sg(st % 8), fq(st / 8), wk(st / RB), ws(st % RB), k0(k0_), nk(nk_),
+          xl(st < NX), wlane(st < CPW * RB), c0(c0_), c1(c1_) {
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                mu[kk][i] = xl && kk < nk ? a.means[(int64_t)(k0 + kk) * D + 4 * fq + i] : 0.0f;
+    }
+    __device__ __forceinline__ void load(int u, int blk) {
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+        const float *src = a.x + (b + 4 * sg) * D + 4 * fq;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            xv[u][t] = xl && b + 4 * sg + t < c1 ? *reinterpret_cast<const f32x4 *>(src + t * D)
+                                                 : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int64_t wrow = b + ws;
+        wl[u] = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
+    }
+    __device__ __forceinline__ void stage(float *img, int u, int blk) const {
+        float *buf = img + (blk % C::NBUF) * C::BUF;
+        if (xl) {
+#pragma unroll
+            for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    f32x4 xb;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) xb[t] = xv[u][t][i] - mu[kk][i];
+                    *reinterpret_cast<f32x4 *>(buf + kk * C::IMG + cov16_off<D>(4 * fq + i, sg)) = xb;
+                }
+        }
+        if (wlane) buf[C::WOFF + wk * RB + ws] = wl[u];
+    }
+};
+
+// d = 64 (and k_gmm_cov_async's layout): thread owns column sc and samples SPT sp .. SPT sp + SPT
+// - 1 of a block; lane l < SPT * CPW also carries one weight
+template <int D>
+struct Cov16StageCol {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    static constexpr int RB = C::RB, CPW = C::CPW, SPT = RB * D / 256;
+    static_assert(SPT % 4 == 0 && SPT * CPW <= 64 && D % 64 == 0, "staging layout");
+    const CovArgs &a;
+    const int sc, sp, wk, ws, k0, nk;
+    const bool wlane;
+    const int64_t c0, c1;
+    float mu[CPW];
+    float xv[3][SPT];
+    float wl[3];
+    __device__ __forceinline__ Cov16StageCol(const CovArgs &a_, int st, int lane, int k0_, int nk_,
+                                             int64_t c0_, int64_t c1_)
+        : a(a_), sc(st % D), sp(st / D), wk(lane / SPT), ws(lane % SPT), k0(k0_), nk(nk_),
+          wlane(lane < SPT * CPW), c0(c0_), c1(c1_) {
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+            mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
+    }
+    __device__ __forceinline__ void load(int u, int blk) {
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+        const float *src = a.x + (b + SPT * sp) * D + sc;
+        if (b + RB <= c1) {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) xv[u][q] = src[q * D];
+        } else {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) xv[u][q] = b + SPT * sp + q < c1 ? src[q * D] : 0.0f;
+        }
+        const int64_t wrow = b + SPT * sp + ws;
+        wl[u] = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
+    }
+    __device__ __forceinline__ void stage(float *img, int u, int blk) const {
+        float *buf = img + (blk % C::NBUF) * C::BUF;
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+            for (int j = 0; j < SPT / 4; ++j) {
+                f32x4 xb;
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) xb[q4] = xv[u][4 * j + q4] - mu[kk];
+                *reinterpret_cast<f32x4 *>(buf + kk * C::IMG + cov16_off<D>(sc, (SPT * sp + 4 * j) / 4)) =
+                    xb;
+            }
+        if (wlane) buf[C::WOFF + wk * RB + SPT * sp + ws] = wl[u];
+    }
+};
+
+// the staging pipeline: block j + 1 is staged while block j is multiplied (two image buffers, one
+// barrier per block); register set (j + 1) % 3 holds block j + 1, reloaded with block j + 4
+template <int D, typename S>
+__device__ __forceinline__ void cov16_staging(float *img, S &sg, int nb) {
+    if (nb == 0) return;
+    constexpr int SD = Cov16<D>::NBUF - 1;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+        if (u < nb) sg.load(u, u);
+#if COME_COV_DIAG == 2
+    sg.stage(img, 0, 0);
+    __syncthreads();
+    return;
+#endif
+    sg.stage(img, 0, 0);
+    if (3 < nb && COME_COV_DIAG != 1) sg.load(0, 3);
+    __syncthreads();  // barrier 0
+    for (int j0 = 0; j0 < nb; j0 += 3) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
+            const int j = j0 + u;
+            if (j >= nb) break;
+            if (j + SD < nb) {
+                sg.stage(img, (u + SD) % 3, j + SD);
+                if (j + SD + 3 < nb && COME_COV_DIAG != 1) sg.load((u + SD) % 3, j + SD + 3);
+            }
+            if (j + 1 < nb) __syncthreads();  // barrier j + 1
+        }
+    }
+}
+
 template <int D>
 __global__ void __launch_bounds__((Cov16<D>::THREADS))
     __attribute__((amdgpu_waves_per_eu(4))) k_gmm_cov16(CovArgs a) {
     using C = Cov16<D>;
     constexpr int CPW = C::CPW;
-    constexpr int NST = 256;  // staging threads (4 wavefronts)
     constexpr int RB = C::RB;
-    constexpr int SPT = RB * D / NST;  // samples staged per thread (16 at d = 128, 8 at d = 64)
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    static_assert(SPT % 4 == 0 && SPT * CPW <= 64 && D % 64 == 0, "staging layout");
     static_assert(C::NBUF * C::BUF * sizeof(float) * 2 <= 160 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) float img[C::NBUF * C::BUF];
+    const int64_t chunk = blockIdx.y;
     const int k0 = blockIdx.x * CPW;
     const int nk = a.K - k0 < CPW ? a.K - k0 : CPW;
-    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    const int64_t c0 = chunk * a.rows_per_chunk;
     int64_t c1 = c0 + a.rows_per_chunk;
     if (c1 > a.V) c1 = a.V;
     const int nb = c1 > c0 ? (int)((c1 - c0 + RB - 1) / RB) : 0;
@@ -1682,69 +1847,18 @@ __global__ void __launch_bounds__((Cov16<D>::THREADS))
         // ---- MFMA wavefronts: component tk, tile part p ----
         const int tk = wid / C::WPC, p = wid % C::WPC;
         constexpr int P1 = C::WPC > 1 ? 1 : 0;
-        if (p == 0) cov16_part<D, 0>(a, img, nb, tk, nk, k0, lane);
-        else cov16_part<D, P1>(a, img, nb, tk, nk, k0, lane);
+        if (p == 0) cov16_part<D, 0>(a, img, nb, tk, nk, k0, chunk, lane);
+        else cov16_part<D, P1>(a, img, nb, tk, nk, k0, chunk, lane);
         return;
     }
-    // ---- staging wavefronts (as k_gmm_cov_async): thread owns column sc and samples SPT sp ..
-    // SPT sp + SPT - 1 of a block; lane l < SPT * CPW also carries one weight ----
+    // ---- staging wavefronts: 16-byte loads at d = 128, one column per thread at d = 64 ----
     const int st = tid - 64 * C::AW;
-    const int sc = st % D, sp = st / D;
-    float mu[CPW];
-#pragma unroll
-    for (int kk = 0; kk < CPW; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
-    float xv[3][SPT];
-    float wl[3];
-    const int wk = lane / SPT, ws = lane % SPT;
-    const bool wlane = lane < SPT * CPW;
-    auto load = [&](int blk, float (&xr)[SPT], float &wr) {
-        const int64_t b = c0 + (int64_t)blk * RB;
-        const float *src = a.x + (b + SPT * sp) * D + sc;
-        if (b + RB <= c1) {
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) xr[q] = src[q * D];
-        } else {
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) xr[q] = b + SPT * sp + q < c1 ? src[q * D] : 0.0f;
-        }
-        const int64_t wrow = b + SPT * sp + ws;
-        wr = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
-    };
-    auto stage = [&](int blk, const float (&xr)[SPT], float wr) {
-        float *buf = img + (blk % C::NBUF) * C::BUF;
-#pragma unroll
-        for (int kk = 0; kk < CPW; ++kk)
-#pragma unroll
-            for (int j = 0; j < SPT / 4; ++j) {
-                f32x4 xb;
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) xb[q4] = xr[4 * j + q4] - mu[kk];
-                *reinterpret_cast<f32x4 *>(buf + kk * C::IMG +
-                                           cov16_off<D>(sc, (SPT * sp + 4 * j) / 4)) = xb;
-            }
-        if (wlane) buf[C::WOFF + wk * RB + SPT * sp + ws] = wr;
-    };
-    if (nb == 0) return;
-    constexpr int SD = C::NBUF - 1;  // block j + 1 is staged while block j is multiplied
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-        if (u < nb) load(u, xv[u], wl[u]);
-    if (0 < nb) {
-        stage(0, xv[0], wl[0]);
-        if (3 < nb) load(3, xv[0], wl[0]);
-    }
-    __syncthreads();  // barrier 0
-    for (int j0 = 0; j0 < nb; j0 += 3) {
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
-            const int j = j0 + u;
-            if (j >= nb) break;
-            if (j + SD < nb) {
-                stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-                if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-            }
-            if (j + 1 < nb) __syncthreads();  // barrier j + 1
-        }
+    if constexpr (D == 128) {
+        Cov16StageX4<D> sg(a, st, k0, nk, c0, c1);
+        cov16_staging<D>(img, sg, nb);
+    } else {
+        Cov16StageCol<D> sg(a, st, lane, k0, nk, c0, c1);
+        cov16_staging<D>(img, sg, nb);
     }
 }
 

@@ -821,13 +821,12 @@ __global__ void __launch_bounds__(128) k_sgns_o2_ring(O2Args a) {
 // Wavefronts per SIMD the stream kernel is compiled for: the kernel is latency-bound (one pair of
 // loads in flight per wavefront), so at d <= 128, n <= 5 it is held to 64 VGPRs for 8 waves per
 // SIMD (a 32-byte spill): 108 vs 119 ms per C3 launch at the 7 waves 70 VGPRs would give
-// (profiles/r02_ab_stream_occupancy.txt).  Wider rows / more negatives keep their natural size.
-#ifndef COME_WIDE_STREAM_WAVES
-#define COME_WIDE_STREAM_WAVES 1  // A/B builds only (scripts/ab_c5_waves.sh)
-#endif
+// (profiles/r02_ab_stream_occupancy.txt).  Wider rows / more negatives keep their natural size:
+// C5's <4, true, 10> held to 4 waves per SIMD ran 3.57 vs 2.10 s per 1M-walk launch
+// (profiles/r05_ab_c5_waves.txt).
 template <int VEC, int MAXN>
 constexpr int stream_waves_per_eu() {
-    return (VEC <= 2 && MAXN <= 5) ? 8 : (VEC == 4 && MAXN == 10) ? COME_WIDE_STREAM_WAVES : 1;
+    return (VEC <= 2 && MAXN <= 5) ? 8 : 1;
 }
 
 template <int VEC, bool FULL, int MAXN>

@@ -100,14 +100,33 @@ def resp_sum(resp, chunks=256):
     return part
 
 
+def scatter_chunks(V, K, d, cus):
+    """Row chunks of the scatter's grid.  The MFMA kernels (d = 64, 128) run (K / components per
+    workgroup) x chunks workgroups, two resident per CU: the chunk count makes that a whole number
+    of rounds of the 2 x CUs slots, 8 of them (~4k workgroups: enough to even out, the partials
+    <= 512 MB).  A ragged last round costs its whole length: at C4 (25 component pairs) 163
+    chunks = 7.96 rounds ran 7.44 ms, 168 (-> 169 used) = 8.25 rounds 7.75 ms
+    (profiles/r05_ab_gmm_diag.txt).  Other widths (the VALU kernel): ~8192 workgroups."""
+    cap = max(1, min((128 << 20) // max(1, K * d * d), -(-V // 64)))
+    if d not in (64, 128) or cus <= 0:
+        return max(1, min(-(-8192 // K), cap))
+    groups = -(-K // (2 if d == 128 else 4))
+    slots = 2 * cus
+    for rounds in range(8, 0, -1):
+        c = rounds * slots // groups
+        if 1 <= c <= cap:
+            return c
+    return max(1, min(cap, slots // groups))
+
+
 def scatter(X, resp, means, chunks=None):
     """[K, d, d] device fp32: sum_i resp[i,k] (x_i - means_k)(x_i - means_k)^T."""
     import torch
     V, d = X.shape
     K = resp.shape[1]
-    if chunks is None:  # ~8192 workgroups, partials <= 512 MB (profiles/r01h_ab_scatter.txt:
-        # at C4, 1000 / 4000 / 8000 workgroups -> 13.0 / 11.9 / 11.5 ms)
-        chunks = max(1, min(-(-8192 // K), (128 << 20) // max(1, K * d * d), -(-V // 64)))
+    if chunks is None:
+        cus = torch.cuda.get_device_properties(X.device).multi_processor_count
+        chunks = scatter_chunks(V, K, d, cus)
     out = torch.empty((K, d, d), dtype=torch.float32, device=X.device)
     scratch = torch.empty((chunks * K * d * d,) if chunks > 1 else (1,), dtype=torch.float32,
                           device=X.device)

@@ -234,3 +234,23 @@ def test_chung_lu_device_path_equals_numpy():
         b = chung_lu(V, deg, seed=4, device=torch.device("cpu"))
         for n in ("edges", "col", "rowptr", "degree"):
             np.testing.assert_array_equal(getattr(a, n), getattr(b, n), err_msg=n)
+
+
+@pytest.mark.parametrize("V,K,d", [(1_000_000, 50, 128), (1_000_000, 7, 128), (100_000, 50, 128),
+                                   (1_000_000, 50, 64), (5000, 3, 64), (1000, 3, 128),
+                                   (2_000_000, 200, 128), (999, 3, 96)])
+def test_scatter_chunks_fill_whole_rounds(V, K, d):
+    """gmm.scatter's default chunk count: the MFMA grid ((K / components per workgroup) x chunks,
+    two workgroups per CU) makes at most 8 whole rounds of the 2 x 256 slots, the partials stay
+    within 512 MB and no chunk is smaller than 64 rows."""
+    from come_amd.gmm import scatter_chunks
+    c = scatter_chunks(V, K, d, 256)
+    assert 1 <= c <= max(1, -(-V // 64))
+    assert c * K * d * d <= max(128 << 20, K * d * d)
+    if d in (64, 128):
+        groups = -(-K // (2 if d == 128 else 4))
+        assert groups * c <= 8 * 512
+        if V >= 64 * 8 * 512:  # rows enough for every slot: whole rounds, within one group
+            assert (groups * c) % 512 > 512 - groups or (groups * c) % 512 == 0
+    if (V, K, d) == (1_000_000, 50, 128):
+        assert c == 163  # = the measured C4 grid (7.96 rounds, profiles/r05_ab_gmm_diag.txt)
