@@ -262,7 +262,7 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       per wavefront, 4 waves per SIMD; 11.57 vs 12.46 ms at C4); 1 = the 32x32x2
  *                       fallback k_community_async.  Other values: COME_E_INVALID
  *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 3 = k_gmm_cov16 (16x16x4
- *                       tiles: 36 of 64 upper tiles at d = 128; 7.27 vs 7.92 ms at C4); 1 = the
+ *                       tiles: 36 of 64 upper tiles at d = 128; 7.25 vs 7.92 ms at C4); 1 = the
  *                       32x32 fallback k_gmm_cov_async.  Other values: COME_E_INVALID
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
  *                       0 = one store per lane per step (identical walks)

@@ -40,6 +40,10 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #ifndef COME_RESP_DIAG
 #define COME_RESP_DIAG 0
 #endif
+// k_gmm_cov16 at d = 128: staging register sets (3 / 4 / 5+: 7.266 / 7.247 ms at C4 / spills)
+#ifndef COME_COV_NS
+#define COME_COV_NS 4
+#endif
 constexpr int kThreads = 256;
 
 // out[r][c] = sum_j A[r][j] * B(c, j) for the tile, where B(c, j) = Bm[c*d + j] (TRANS=false,
@@ -1690,8 +1694,8 @@ __device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, i
 // d = 128: 16-byte loads.  Thread st < RB D / 16 owns feature quad fq = st / 8 (features 4 fq ..
 // 4 fq + 3) of samples 4 sg .. 4 sg + 3, sg = st % 8: one dwordx4 per sample, 8 lanes reading one
 // 128-B line; each feature's 4 samples become one b128 granule (8 consecutive lanes write the 8
-// granules of one image row: conflict-free).  Thread st < CPW RB carries the weight of sample
-// st % RB for component st / RB.  (vs one dword per column and sample: 7.27 vs 7.40 ms at C4,
+// granules of one image row: conflict-free).  Thread st carries the weight of sample st % RB for
+// component st % (CPW RB) / RB (four threads per weight, the same value: no branch).  (vs one dword per column and sample: 7.27 vs 7.40 ms at C4,
 // bit-identical, profiles/r05_ab_gmm_diag.txt; the d = 64 form below needs too many registers this
 // way: 16 means per thread.)
 template <int D>
@@ -1704,48 +1708,59 @@ struct Cov16StageX4 {
     const int sg, fq, wk, ws, k0, nk;
     const bool xl, wlane;
     const int64_t c0, c1;
+    static constexpr int NS = COME_COV_NS;  // register sets: loads run NS blocks ahead
     float mu[CPW][4];
-    f32x4 xv[3][4];
-    float wl[3];
+    f32x4 xv[NS][4];
+    float wl[NS];
     __device__ __forceinline__ Cov16StageX4(const CovArgs &a_, int st, int k0_, int nk_, int64_t c0_,
                                             int64_t c1_)
-        : a(a_), sg(st % 8), fq(st / 8), wk(st / RB), ws(st % RB), k0(k0_), nk(nk_),
-          xl(st < NX), wlane(st < CPW * RB), c0(c0_), c1(c1_) {
+        : a(a_), sg(st % 8), fq(st / 8), wk(st % (CPW * RB) / RB), ws(st % RB), k0(k0_), nk(nk_),
+          xl(st < NX), wlane(true), c0(c0_), c1(c1_) {
 #pragma unroll
         for (int kk = 0; kk < CPW; ++kk)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 mu[kk][i] = xl && kk < nk ? a.means[(int64_t)(k0 + kk) * D + 4 * fq + i] : 0.0f;
     }
+    // Loads are unconditional (rows past the chunk clamped to its last row, components past K
+    // to K - 1) and the out-of-range values zeroed when staged: a load under a divergent branch
+    // leaves the compiler unable to count the loads in flight, and it then waits for all of them
+    // (vmcnt(0)) before every stage -- the three-block lookahead collapses to none.
     __device__ __forceinline__ void load(int u, int blk) {
         const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
-        const float *src = a.x + (b + 4 * sg) * D + 4 * fq;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-            xv[u][t] = xl && b + 4 * sg + t < c1 ? *reinterpret_cast<const f32x4 *>(src + t * D)
-                                                 : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        const int64_t wrow = b + ws;
-        wl[u] = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
+        for (int t = 0; t < 4; ++t) {
+            const int64_t r = min(b + 4 * sg + t, c1 - 1);
+            xv[u][t] = *reinterpret_cast<const f32x4 *>(a.x + r * D + 4 * fq);
+        }
+        const int64_t wrow = min(b + ws, c1 - 1);
+        wl[u] = a.resp[wrow * a.K + min(k0 + wk, a.K - 1)];
     }
     __device__ __forceinline__ void stage(float *img, int u, int blk) const {
         float *buf = img + (blk % C::NBUF) * C::BUF;
-        if (xl) {
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+        // (the values are read outside any branch: a register read under a divergent branch
+        // also makes the compiler drain every load in flight)
+        const float w = wk < nk && b + ws < c1 ? wl[u] : 0.0f;
+        if (NX == 256 || xl) {  // every thread holds samples at d = 128 (no branch)
 #pragma unroll
             for (int kk = 0; kk < CPW; ++kk)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     f32x4 xb;
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) xb[t] = xv[u][t][i] - mu[kk][i];
+                    for (int t = 0; t < 4; ++t)
+                        xb[t] = b + 4 * sg + t < c1 ? xv[u][t][i] - mu[kk][i] : 0.0f;
                     *reinterpret_cast<f32x4 *>(buf + kk * C::IMG + cov16_off<D>(4 * fq + i, sg)) = xb;
                 }
         }
-        if (wlane) buf[C::WOFF + wk * RB + ws] = wl[u];
+        buf[C::WOFF + wk * RB + ws] = w;  // (threads st, st + 64, ... write the same value)
     }
 };
 
 // d = 64 (and k_gmm_cov_async's layout): thread owns column sc and samples SPT sp .. SPT sp + SPT
-// - 1 of a block; lane l < SPT * CPW also carries one weight
+// - 1 of a block; lane l also carries the weight of sample SPT sp + l % SPT for component
+// l % (SPT CPW) / SPT
 template <int D>
 struct Cov16StageCol {
     using C = Cov16<D>;
@@ -1756,72 +1771,73 @@ struct Cov16StageCol {
     const int sc, sp, wk, ws, k0, nk;
     const bool wlane;
     const int64_t c0, c1;
+    static constexpr int NS = 3;
     float mu[CPW];
     float xv[3][SPT];
     float wl[3];
     __device__ __forceinline__ Cov16StageCol(const CovArgs &a_, int st, int lane, int k0_, int nk_,
                                              int64_t c0_, int64_t c1_)
-        : a(a_), sc(st % D), sp(st / D), wk(lane / SPT), ws(lane % SPT), k0(k0_), nk(nk_),
-          wlane(lane < SPT * CPW), c0(c0_), c1(c1_) {
+        : a(a_), sc(st % D), sp(st / D), wk(lane % (SPT * CPW) / SPT), ws(lane % SPT), k0(k0_),
+          nk(nk_), wlane(true), c0(c0_), c1(c1_) {
 #pragma unroll
         for (int kk = 0; kk < CPW; ++kk)
             mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
     }
+    // unconditional loads, out-of-range values zeroed when staged (as Cov16StageX4)
     __device__ __forceinline__ void load(int u, int blk) {
         const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
-        const float *src = a.x + (b + SPT * sp) * D + sc;
-        if (b + RB <= c1) {
 #pragma unroll
-            for (int q = 0; q < SPT; ++q) xv[u][q] = src[q * D];
-        } else {
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) xv[u][q] = b + SPT * sp + q < c1 ? src[q * D] : 0.0f;
-        }
-        const int64_t wrow = b + SPT * sp + ws;
-        wl[u] = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
+        for (int q = 0; q < SPT; ++q) xv[u][q] = a.x[min(b + SPT * sp + q, c1 - 1) * D + sc];
+        const int64_t wrow = min(b + SPT * sp + ws, c1 - 1);
+        wl[u] = a.resp[wrow * a.K + min(k0 + wk, a.K - 1)];
     }
     __device__ __forceinline__ void stage(float *img, int u, int blk) const {
         float *buf = img + (blk % C::NBUF) * C::BUF;
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
 #pragma unroll
         for (int kk = 0; kk < CPW; ++kk)
 #pragma unroll
             for (int j = 0; j < SPT / 4; ++j) {
                 f32x4 xb;
 #pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) xb[q4] = xv[u][4 * j + q4] - mu[kk];
+                for (int q4 = 0; q4 < 4; ++q4)
+                    xb[q4] = b + SPT * sp + 4 * j + q4 < c1 ? xv[u][4 * j + q4] - mu[kk] : 0.0f;
                 *reinterpret_cast<f32x4 *>(buf + kk * C::IMG + cov16_off<D>(sc, (SPT * sp + 4 * j) / 4)) =
                     xb;
             }
-        if (wlane) buf[C::WOFF + wk * RB + SPT * sp + ws] = wl[u];
+        const float w = wk < nk && b + SPT * sp + ws < c1 ? wl[u] : 0.0f;
+        buf[C::WOFF + wk * RB + SPT * sp + ws] = w;  // (lanes l, l + SPT CPW: the same value)
     }
 };
 
 // the staging pipeline: block j + 1 is staged while block j is multiplied (two image buffers, one
-// barrier per block); register set (j + 1) % 3 holds block j + 1, reloaded with block j + 4
+// barrier per block); register set (j + 1) % NS holds block j + 1, reloaded with block j + 1 + NS.
+// Every load and stage is issued unconditionally (the block index clamped to nb - 1; a stage of
+// block nb lands in a buffer nobody reads again, its values zeroed): with no branch around them
+// the compiler counts the loads in flight exactly and each stage waits only for its own set
+// (a conditional load made it drain all of them, vmcnt(0), at the loop head).
 template <int D, typename S>
 __device__ __forceinline__ void cov16_staging(float *img, S &sg, int nb) {
     if (nb == 0) return;
-    constexpr int SD = Cov16<D>::NBUF - 1;
+    constexpr int SD = Cov16<D>::NBUF - 1, NS = S::NS;
+    const int last = nb - 1;
 #pragma unroll
-    for (int u = 0; u < 3; ++u)
-        if (u < nb) sg.load(u, u);
+    for (int u = 0; u < NS; ++u) sg.load(u, min(u, last));
 #if COME_COV_DIAG == 2
     sg.stage(img, 0, 0);
     __syncthreads();
     return;
 #endif
     sg.stage(img, 0, 0);
-    if (3 < nb && COME_COV_DIAG != 1) sg.load(0, 3);
+    if (COME_COV_DIAG != 1) sg.load(0, min(NS, last));
     __syncthreads();  // barrier 0
-    for (int j0 = 0; j0 < nb; j0 += 3) {
+    for (int j0 = 0; j0 < nb; j0 += NS) {
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {  // j = j0 + u: register set (j + SD) % 3
+        for (int u = 0; u < NS; ++u) {  // j = j0 + u: register set (j + SD) % NS
             const int j = j0 + u;
-            if (j >= nb) break;
-            if (j + SD < nb) {
-                sg.stage(img, (u + SD) % 3, j + SD);
-                if (j + SD + 3 < nb && COME_COV_DIAG != 1) sg.load((u + SD) % 3, j + SD + 3);
-            }
+            if (j >= nb) return;  // (not break: the loop head then sees one load order only)
+            sg.stage(img, (u + SD) % NS, j + SD);
+            if (COME_COV_DIAG != 1) sg.load((u + SD) % NS, min(j + SD + NS, last));
             if (j + 1 < nb) __syncthreads();  // barrier j + 1
         }
     }
