@@ -33,7 +33,9 @@ constexpr int kTR = 16;        // rows per workgroup tile
 // COME_COV_DIAG 1 = staging re-stages the first 3 blocks' registers (no global loads after the
 // prologue), 2 = MFMA wavefronts consume buffer 0 without barriers (the MFMA stream alone), 3 =
 // every load reads the chunk's first block (the same instructions, cache-resident data).
-// COME_RESP_DIAG (k_gmm_resp16t) 1 = no copies after component 0, 2 = and no barriers.
+// COME_RESP_DIAG (k_gmm_resp16t) 1 = no copies after component 0, 2 = and no barriers (both read
+// the never-written second buffer for odd components: zero-like data, which clocks higher), 3 /
+// 4 = as 1 / 2 with every component read from buffer 0 (real data: component 0 repeated).
 #ifndef COME_COV_DIAG
 #define COME_COV_DIAG 0
 #endif
@@ -1046,6 +1048,8 @@ __global__ void __launch_bounds__(256) k_pack_upper16(const float *__restrict__ 
 // One 16-row tile per wavefront, 8 wavefronts per 128-row workgroup (91-95 VGPRs: 4 waves per
 // SIMD -- the LDS holds two workgroups per CU either way); two row tiles per wavefront and 4
 // wavefronts (216 VGPRs, 2 waves per SIMD) were bit-identical and 1.5% slower (7.10 vs 7.00 ms).
+// (16 wavefronts = 256-row workgroups, one per CU, half the component copies per row: 7.37 vs
+// 7.00 ms -- the second workgroup's cover at barriers is worth more; profiles/r05_ab_gmm_diag.txt)
 struct R16tShape {
     static constexpr int NW = 8;                 // wavefronts per workgroup
     static constexpr int ROWS = 16 * NW;         // rows per workgroup (128)
@@ -1191,20 +1195,21 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
     for (int k = 0; k < a.K; ++k) {
         if (k + 1 < a.K && !COME_RESP_DIAG)
             r16t_stage<D>(a, k + 1, T::blocks(sm, k + 1), T::slot(sm, k + 1), wid, lane);
+        const int kb = COME_RESP_DIAG >= 3 ? 0 : k;  // the buffer read
         // component k - 1's log-probability is stored one component late: a store counts on the
         // vector-memory counter like the staging copies, so storing it right before the barrier's
         // vmcnt(0) made every wavefront wait out the store's round trip once per component
         if (k > 0 && owner) a.resp[my_row * a.K + k - 1] = lp_prev;
-        const float *par = T::slot(sm, k);
+        const float *par = T::slot(sm, kb);
         f32x4 acc[NQ];
-        r16t_blocks<D>(xb, T::blocks(sm, k), abase, acc);
+        r16t_blocks<D>(xb, T::blocks(sm, kb), abase, acc);
         float sq = 0.0f;
 #pragma unroll
         for (int ct = 0; ct < NQ; ++ct) r16t_sq<D>(acc[ct], par, ct, kg, sq);
         const float lp = r16t_lp_of<D>(sq, par);
         lse_push(lp, run_max, run_sum);
         lp_prev = lp;
-#if COME_RESP_DIAG != 2
+#if COME_RESP_DIAG != 2 && COME_RESP_DIAG != 4
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // buffer k & 1 free; component k + 1 in the other buffer
 #endif
@@ -2217,7 +2222,8 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
                 attr16t = true;
             }
             hipLaunchKernelGGL(d == 64 ? k_gmm_resp16t<64> : k_gmm_resp16t<128>,
-                               dim3((unsigned)((V + 127) / 128)), dim3(R16tShape::THREADS), ldst,
+                               dim3((unsigned)((V + R16tShape::ROWS - 1) / R16tShape::ROWS)),
+                               dim3(R16tShape::THREADS), ldst,
                                (hipStream_t)stream, b);
             rc = hip_error(hipGetLastError(), "k_gmm_resp16t launch");
             if (rc) return rc;
