@@ -71,19 +71,27 @@ def secondary_rows(timeout_s=150):
     bench_aux.py in a child process (one JSON line each, with its bounded CPU baseline: the O1
     Hogwild restatement for ~6 s plus its reference-equivalent rate, the reference's numpy
     community loop and one sklearn EM iteration on row samples; none for the walker):
-    C2 O1 pass, C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass.
+    C2 O1 pass, C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass, and
+    one GPU's share of configs[4]/C5 (this script on the 10M-node graph at d = 256, n = 10: one
+    1,048,576-walk launch per step over full-size replicated tables, what each of C5's 8 ranks
+    runs; no CPU baseline -- host copies of its 20 GB of tables).
     Outside the timed region and never part of `value`; a failing row is reported as an error
     string."""
     import subprocess
     out = {}
-    for wl in ("c2", "c4", "walks"):
+    for wl in ("c2", "c4", "walks", "c5"):
         cmd = [sys.executable, os.path.join(ROOT, "bench_aux.py"), "--workload", wl,
                "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]
         if wl == "walks":  # its baseline walks a full corpus pass per thread (~20 s): skipped
             cmd.append("--no-cpu-baseline")
+        if wl == "c5":
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--nodes", "10000000",
+                   "--dim", "256", "--negative", "10", "--steps", "3", "--warmup", "1",
+                   "--no-secondary", "--no-cpu-baseline"]
         t0 = time.time()
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+            r = subprocess.run(cmd, capture_output=True, text=True,
+                               timeout=timeout_s * (2 if wl == "c5" else 1))
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             if r.returncode != 0 or not line:
                 out[wl] = "error rc=%d: %s" % (r.returncode, r.stderr.strip()[-300:])
@@ -94,6 +102,9 @@ def secondary_rows(timeout_s=150):
                    "roofline_frac": j["roofline"]["frac"], "roofline_bound": j["roofline"]["bound"],
                    "avg_kernel_ms": j["roofline"]["avg_kernel_ms"], "wall_s": time.time() - t0,
                    "cpu_baseline": j.get("cpu_baseline")}
+            if wl == "c5":
+                for k in ("frac_skip_adjusted", "bytes_per_pair_skip_adjusted"):
+                    row[k] = j["roofline"].get(k)
             if wl == "c4":
                 for k in ("gmm_resp_kernel", "gmm_resp_ms", "gmm_resp_tflops_executed",
                           "gmm_scatter_ms",
@@ -383,7 +394,7 @@ def main():
 
     secondary = None
     if world == 1 and not args.no_secondary:
-        log("secondary rows (bench_aux.py c2 / c4 / walks, outside the timed region)")
+        log("secondary rows (bench_aux.py c2 / c4 / walks, bench.py C5 shard; outside the timed region)")
         secondary = secondary_rows()
 
     sync_measure = None
