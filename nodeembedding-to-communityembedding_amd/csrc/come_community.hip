@@ -1081,6 +1081,27 @@ __device__ __forceinline__ void r16t_stage(const RespArgs &a, int k, float *buf,
     }
 }
 
+// piece j of r16t_stage's copy (j = 0 also copies mu_k P_k and the parameters), for the copy
+// spread over the MFMA stream (k_gmm_resp16t)
+template <int D>
+__device__ __forceinline__ void r16t_stage_piece(const RespArgs &a, int k, float *buf, float *par,
+                                                 int wid, int lane, int j) {
+    using T = Resp16T<D>;
+    constexpr int NW = R16tShape::NW;
+    const float *src = a.prec_t + (int64_t)k * T::TRI;
+    const int i = wid + NW * j;
+    if (i < T::PIECES)  // wavefront-uniform
+        __builtin_amdgcn_global_load_lds(src + i * 256 + lane * 4, buf + i * 256, 16, 0, 0);
+    if (j == 0 && wid == 0) {
+        const int s = lane * 4 < D ? lane * 4 : D - 4;
+        __builtin_amdgcn_global_load_lds(a.mu_prec + (int64_t)k * D + s, par + T::MP, 16, 0, 0);
+    } else if (j == 0 && wid == 1) {
+        const float *p = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
+                                   : a.log_norm + k;
+        __builtin_amdgcn_global_load_lds(p, par + T::PAR, 4, 0, 0);
+    }
+}
+
 // Block n of the upper triangle in row-major order (q, ct >= q), as compile-time tables.
 template <int NQ>
 struct TriBlocks {
@@ -1102,10 +1123,10 @@ struct TriBlocks {
 // blocks in pairs with interleaved accumulation chains +0.5%; the next component's staging issued
 // behind the first A reads 0; a packed-fp32 epilogue 0; the accumulators started at -mu_k P_k and
 // the log-sum-exp after the loop: no gain -- profiles/r04_ab_estep16.txt.)
-template <int D>
+template <int D, typename Hook>
 __device__ __forceinline__ void r16t_blocks(
     const __attribute__((ext_vector_type(4))) float (&xb)[D / 16], const float *buf, int abase,
-    __attribute__((ext_vector_type(4))) float (&acc)[D / 16]) {
+    __attribute__((ext_vector_type(4))) float (&acc)[D / 16], Hook &&hook) {
     using T = Resp16T<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr int NQ = T::NQ;
@@ -1122,6 +1143,7 @@ __device__ __forceinline__ void r16t_blocks(
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
         if (n + 2 < NB) av[(n + 2) % 3] = fetch(n + 2);
+        hook(n);  // other work placed beside this block's MFMAs
         const int q = TB.q[n], ct = TB.ct[n];
         // quad 0's blocks (n < NQ) start acc[ct] from zero: the accumulator is born here
         if (q == 0) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1193,8 +1215,6 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
     const bool owner = kg == 0 && my_row < a.V;
     float run_max = -INFINITY, run_sum = 0.0f, lp_prev = 0.0f;
     for (int k = 0; k < a.K; ++k) {
-        if (k + 1 < a.K && !COME_RESP_DIAG)
-            r16t_stage<D>(a, k + 1, T::blocks(sm, k + 1), T::slot(sm, k + 1), wid, lane);
         const int kb = COME_RESP_DIAG >= 3 ? 0 : k;  // the buffer read
         // component k - 1's log-probability is stored one component late: a store counts on the
         // vector-memory counter like the staging copies, so storing it right before the barrier's
@@ -1202,7 +1222,20 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
         if (k > 0 && owner) a.resp[my_row * a.K + k - 1] = lp_prev;
         const float *par = T::slot(sm, kb);
         f32x4 acc[NQ];
-        r16t_blocks<D>(xb, T::blocks(sm, kb), abase, acc);
+        // component k + 1's copy (4-5 1-KiB LDS-DMA pieces per wavefront at d = 128) issued one
+        // piece every SP blocks from block 3 instead of all at the component's head, where they sat
+        // on the MFMA ramp: 6.95 vs 7.01 ms at C4 (SP = 7) (spacing 2 / 4 / 8 / 6 from block 4: 7.01 / 6.99 / 6.99 /
+        // 6.95; profiles/r05_ab_gmm_diag.txt)
+        r16t_blocks<D>(xb, T::blocks(sm, kb), abase, acc, [&](int n) {
+            constexpr int NB = T::NQ * (T::NQ + 1) / 2, OFF = 3;
+            constexpr int PER = (T::PIECES + R16tShape::NW - 1) / R16tShape::NW;
+            constexpr int SP = (NB - OFF + PER - 1) / PER;  // 7 at d = 128, 4 at d = 64
+            static_assert(OFF + SP * (PER - 1) < NB, "every piece lands on a block");
+            const int m = n - OFF;
+            if (!COME_RESP_DIAG && m >= 0 && m % SP == 0 && m / SP < PER && k + 1 < a.K)
+                r16t_stage_piece<D>(a, k + 1, T::blocks(sm, k + 1), T::slot(sm, k + 1), wid, lane,
+                                    m / SP);
+        });
         float sq = 0.0f;
 #pragma unroll
         for (int ct = 0; ct < NQ; ++ct) r16t_sq<D>(acc[ct], par, ct, kg, sq);
