@@ -71,10 +71,14 @@ def secondary_rows(timeout_s=150):
     bench_aux.py in a child process (one JSON line each, with its bounded CPU baseline: the O1
     Hogwild restatement for ~6 s plus its reference-equivalent rate, the reference's numpy
     community loop and one sklearn EM iteration on row samples; none for the walker):
-    C2 O1 pass, C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass, and
-    one GPU's share of configs[4]/C5 (this script on the 10M-node graph at d = 256, n = 10: one
-    1,048,576-walk launch per step over full-size replicated tables, what each of C5's 8 ranks
-    runs; no CPU baseline -- host copies of its 20 GB of tables).
+    C2 O1 pass, C4 community pass + GMM E-step / M-step scatter / EM iteration, walker pass (CPU:
+    the exact CPython-stream walker, one corpus pass per host thread), and one GPU's share of
+    configs[4]/C5 (this script on the 10M-node graph at d = 256, n = 10: one 1,048,576-walk launch
+    per step over full-size replicated tables, what each of C5's 8 ranks runs; CPU: the Hogwild
+    restatement for 6 s over host copies of the full 20 GB of tables).  The C5 row's
+    `roofline_frac` is the skip-adjusted fraction (SURVEY.md §8d's 24,576 B per pair counts every
+    target row as written; at C5 most targets are skipped, so that model exceeds the bytes the
+    launch must move and its fraction can pass 1 -- kept as `roofline_frac_all_targets_written`).
     Outside the timed region and never part of `value`; a failing row is reported as an error
     string."""
     import subprocess
@@ -82,12 +86,11 @@ def secondary_rows(timeout_s=150):
     for wl in ("c2", "c4", "walks", "c5"):
         cmd = [sys.executable, os.path.join(ROOT, "bench_aux.py"), "--workload", wl,
                "--steps", "10", "--warmup", "2", "--cpu-seconds", "6"]
-        if wl == "walks":  # its baseline walks a full corpus pass per thread (~20 s): skipped
-            cmd.append("--no-cpu-baseline")
         if wl == "c5":
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--nodes", "10000000",
                    "--dim", "256", "--negative", "10", "--steps", "3", "--warmup", "1",
-                   "--no-secondary", "--no-cpu-baseline"]
+                   "--no-secondary", "--cpu-seconds", "6",
+                   "--traffic-json", os.path.join(ROOT, "profiles", "traffic_c5.json")]
         t0 = time.time()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True,
@@ -103,8 +106,14 @@ def secondary_rows(timeout_s=150):
                    "avg_kernel_ms": j["roofline"]["avg_kernel_ms"], "wall_s": time.time() - t0,
                    "cpu_baseline": j.get("cpu_baseline")}
             if wl == "c5":
-                for k in ("frac_skip_adjusted", "bytes_per_pair_skip_adjusted"):
-                    row[k] = j["roofline"].get(k)
+                rf = j["roofline"]
+                row["roofline_frac"] = rf["frac_skip_adjusted"]
+                row["roofline_frac_all_targets_written"] = rf["frac"]
+                row["bytes_per_pair_skip_adjusted"] = rf["bytes_per_pair_skip_adjusted"]
+                row["achieved_GBps_skip_adjusted"] = rf["achieved_skip_adjusted"]
+                row["traffic"] = rf.get("traffic")
+                if rf.get("traffic"):
+                    row["traffic_GBps"] = rf["traffic"] / (rf["avg_kernel_ms"] / 1e3) / 1e9
             if wl == "c4":
                 for k in ("gmm_resp_kernel", "gmm_resp_ms", "gmm_resp_tflops_executed",
                           "gmm_scatter_ms",

@@ -312,7 +312,8 @@ def walks(args):
     if not args.no_cpu_baseline:
         Gh = gu.Graph(np.arange(1, g.V + 1), g.rowptr, g.col.astype(np.int32), g.degree,
                       np.zeros((0, 2), np.int32))
-        threads = min(16, os.cpu_count() or 1)
+        from oracle import oracle as orc
+        threads = orc.usable_cpus()  # the cgroup quota (16 on the GPU box), not os.cpu_count()
         t0 = time.time()  # one full pass per stream, streams on parallel threads
         w = gu._corpus(Gh, [1] * threads, L, 0.0, [random.Random(s) for s in range(threads)],
                        threads=threads)

@@ -2212,7 +2212,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
     RespArgs a{x, prec_chol, mu_prec, log_norm, resp_out, lse_out, V, d, K, nullptr};
     if (mfma) {
         int *flags = (int *)stream_scratch(dev, stream, kScratchGmmFlags, sizeof(int) * (K + 1));
-        if (!flags) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+        if (!flags) return scratch_failed();
         rc = hip_error(hipMemsetAsync(flags + K, 0, sizeof(int), (hipStream_t)stream),
                        "gmm_resp: flag reset");
         if (rc) return rc;
@@ -2222,7 +2222,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         if (rc) return rc;
         a.lower = flags;
         float *pt = stream_scratch(dev, stream, kScratchGmmPt, sizeof(float) * (size_t)K * d * d);
-        if (!pt) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+        if (!pt) return scratch_failed();
         hipLaunchKernelGGL(k_transpose_sq, dim3((d / 32) * (d / 32), K), dim3(256), 0,
                            (hipStream_t)stream, prec_chol, d, pt);
         rc = hip_error(hipGetLastError(), "k_transpose_sq launch");
@@ -2234,7 +2234,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
             // triangular), then k_gmm_resp16_full (a no-op unless some factor is lower or dense)
             const int tri = d == 64 ? Resp16T<64>::TRI : Resp16T<128>::TRI;
             float *packed = stream_scratch(dev, stream, kScratchGmmTri, sizeof(float) * (size_t)K * tri);
-            if (!packed) return set_error(COME_E_HIP, "gmm_resp: scratch allocation failed");
+            if (!packed) return scratch_failed();
             hipLaunchKernelGGL(d == 64 ? k_pack_upper16<64> : k_pack_upper16<128>,
                                dim3((unsigned)((tri + 255) / 256), K), dim3(256), 0,
                                (hipStream_t)stream, prec_chol, packed);

@@ -85,16 +85,36 @@ static std::mutex g_scratch_mu;
 // that stream finish first, and no device-wide synchronisation happens in the middle of a stream
 // (a plain hipFree here stalled the device).  Grown by at least 1.5x so a slowly
 // growing caller reallocates O(log) times.
+// A growth inside a stream capture is refused: hipFreeAsync / hipMallocAsync would
+// become graph nodes, and the cache would keep a graph-owned pointer that later eager launches on
+// the stream reuse.  Failures set the error message; callers return scratch_failed().
+static thread_local int g_scratch_rc = COME_OK;
+
+int scratch_failed() { return g_scratch_rc; }
+
 float *stream_scratch(int device, void *stream, int slot, size_t bytes) {
-    if (slot < 0 || slot >= kScratchSlots) return nullptr;
+    if (slot < 0 || slot >= kScratchSlots) {
+        g_scratch_rc = set_error(COME_E_INVALID, "scratch slot %d", slot);
+        return nullptr;
+    }
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     Scratch &s = g_scratch[device][slot][stream];
     if (s.bytes >= bytes) return s.ptr;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess ||
+        cap != hipStreamCaptureStatusNone) {
+        g_scratch_rc = set_error(COME_E_INVALID,
+                                 "library scratch must grow to %zu bytes while the stream is being "
+                                 "captured: run the same call once before capturing it", bytes);
+        return nullptr;
+    }
     if (s.bytes) bytes = std::max(bytes, s.bytes + s.bytes / 2);
     if (s.ptr) (void)hipFreeAsync(s.ptr, (hipStream_t)stream);
     s = Scratch{};
-    if (hipMallocAsync((void **)&s.ptr, bytes, (hipStream_t)stream) != hipSuccess) {
+    const hipError_t e = hipMallocAsync((void **)&s.ptr, bytes, (hipStream_t)stream);
+    if (e != hipSuccess) {
         s.ptr = nullptr;
+        g_scratch_rc = hip_error(e, "library scratch allocation");
         return nullptr;
     }
     s.bytes = bytes;

@@ -112,7 +112,7 @@ int derive_hot_rows(int dev, const uint32_t *table, uint64_t T, int packed, int6
                                                   sizeof(uint32_t) * (size_t)V);
     uint32_t *bits = (uint32_t *)stream_scratch(dev, stream, kScratchHotBits,
                                                 sizeof(uint32_t) * (size_t)((V + 31) / 32));
-    if (!counts || !bits) return set_error(COME_E_HIP, "hot rows: scratch allocation failed");
+    if (!counts || !bits) return scratch_failed();
     uint64_t min_count = (uint64_t)(COME_DEFAULT_HOT_SHARE * (double)T);
     if (min_count < 1) min_count = 1;
     *bits_out = bits;

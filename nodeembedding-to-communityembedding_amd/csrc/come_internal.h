@@ -26,10 +26,12 @@ int num_cus(int device);                        // multiprocessor count (cached)
 int64_t *launch_counter(int device, void *stream);
 // Device scratch of at least `bytes` for launches on `stream` (library-owned, one buffer per
 // device, stream and slot, grows on demand: the first call at a larger size allocates, so capture
-// a stream only after a warm-up call of the same shape).
+// a stream only after a warm-up call of the same shape -- a growth during capture is refused).
+// nullptr on failure, with the error message set: return scratch_failed() (its status code).
 constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchHotCounts = 2, kScratchHotBits = 3,
               kScratchGmmTri = 4, kScratchSlots = 5;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
+int scratch_failed();
 // The contended-row bitmap a Hogwild launch uses when the caller passes none (come_hot.hip):
 // rows holding >= max(1, floor(COME_DEFAULT_HOT_SHARE * T)) slots of `table` (plain uint32 or, with
 // `packed`, come_pack_table's words), written into library scratch on `stream`.

@@ -200,6 +200,29 @@ class _LocalWork(object):
         self.g._complete(self.k)
 
 
+REAL_CHANGE_REL = 2.0 ** -20  # 8 ulps of fp32: above any rounding an exchange leaves behind
+
+
+def _real_change(delta, base):
+    """Per row: does some element of ``delta`` exceed 8 ulps of the same element of ``base``?  A
+    real SGD update of a row moves at least one element by far more than that (even with a
+    decayed learning rate on a large-norm row, its small elements move by many of their own
+    ulps); the residue an overlapped exchange leaves on rows nobody changed is a few ulps."""
+    import torch
+    if isinstance(delta, np.ndarray):
+        v = np.abs(delta.reshape(delta.shape[0], -1).astype(np.float32))
+        b = np.abs(base.reshape(base.shape[0], -1).astype(np.float32))
+        return (v > b * np.float32(REAL_CHANGE_REL)).any(axis=1)
+    v = delta.reshape(delta.shape[0], -1)
+    b = base.reshape(base.shape[0], -1)
+    out = torch.zeros(v.shape[0], dtype=torch.bool, device=v.device)
+    step = max(1, (1 << 24) // max(1, v.shape[1]))  # row blocks: temporaries of <= 64 MB
+    for lo in range(0, v.shape[0], step):
+        hi = min(lo + step, v.shape[0])
+        out[lo:hi] = (v[lo:hi].abs() > b[lo:hi].abs() * REAL_CHANGE_REL).any(dim=1)
+    return out
+
+
 def _fused(t):
     """CUDA fp32 tables with n % 4 == 0 use the fused HIP passes (come_delta_begin/end); CPU
     tensors (gloo tests) use the same arithmetic in torch ops."""
@@ -228,7 +251,7 @@ class DeltaAllReduce(object):
     OVERLAP_SAFE = ("sum", "mean", "touched_mean", "hot_mean")
 
     def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum",
-                 mean_rows=None, pick_rows=None, same_start=True):
+                 mean_rows=None, pick_rows=None, same_start=True, force_exchange=False):
         import torch
         if combine not in self.COMBINES:
             raise ValueError("combine must be one of %s" % (self.COMBINES,))
@@ -243,18 +266,22 @@ class DeltaAllReduce(object):
         self.comm = comm if comm is not None else TorchComm(group)
         self.world = self.comm.world
         self.rank = getattr(self.comm, "rank", 0)
+        # one rank exchanges nothing; force_exchange (tests) runs the whole protocol anyway, so
+        # a one-GPU box drives RCCL's collectives and the stream waits (tests/test_gpu_rccl.py)
+        self.active = self.world > 1 or bool(force_exchange)
         self.bucket = int(bucket_elems)
         self.combine = combine
         self.exchanges = 0
-        if self.world > 1 and same_start:
+        if self.active and same_start:
             self._broadcast()
-        self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
-        self.dsum = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
-        self.down = [torch.empty_like(t) for t in self.tables] if self.world > 1 else None
+        self.snap = [t.clone() for t in self.tables] if self.active else None
+        self.dsum = [torch.empty_like(t) for t in self.tables] if self.active else None
+        self.down = [torch.empty_like(t) for t in self.tables] if self.active else None
         self.cnt = None
         self.prio = None
         self.prepared = False
         self.pending = []
+        self.synced = self.active and same_start  # replicas identical right now
 
     def _broadcast(self):
         """Every replica starts from rank 0's tables: the exchange adds deltas to each rank's own
@@ -262,15 +289,22 @@ class DeltaAllReduce(object):
         for t in self.tables:
             self.comm.broadcast(t, 0)
 
-    def reset(self):
+    def reset(self, broadcast=None):
         """Make the current tables the sync base (W_sync = W), after taking rank 0's tables (the
         replicas must agree).  Call when the tables changed outside the exchange (e.g. another
-        trainer's distributed step), so that change is not counted once per rank as a delta."""
+        trainer's distributed step), so that change is not counted once per rank as a delta.
+        ``broadcast=None``: broadcast only when the replicas may differ -- not after a blocking
+        sync() (which leaves them bit-identical; a trainer's train() ends with one), provided
+        whatever changed the tables since did so identically on every rank, as every distributed
+        step of this package does.  That skips a whole-table broadcast per train() call (2 GB of
+        xGMI traffic per call at C3, 41 GB at C5's shard).  True / False force it."""
         self.finish()
-        if self.world > 1:
-            self._broadcast()
+        if self.active:
+            if broadcast or (broadcast is None and not self.synced):
+                self._broadcast()
             for t, s in zip(self.tables, self.snap):
                 s.copy_(t)
+            self.synced = True
 
     def prepare(self):
         """First half of start(): finish any pending exchange, snapshot this rank's delta
@@ -278,7 +312,7 @@ class DeltaAllReduce(object):
         number of ranks that changed each row; pick: the priority of the rank whose delta a row
         takes).  start() calls it when it has not run; a one-process simulation of N ranks
         (LocalReplicas) calls it on every rank before any rank's start()."""
-        if self.world == 1 or self.prepared:
+        if not self.active or self.prepared:
             return
         import torch
         self.finish()
@@ -306,11 +340,10 @@ class DeltaAllReduce(object):
                 self.pending.append(self.comm.all_reduce(c, async_op=True))
             if pick:
                 # A rank whose change of a row is rounding-level only (an overlapped exchange
-                # leaves W_sync + D_own one rounding away from W on rows nobody else changed) must
-                # not win the row over a rank that trained it: such keys carry bit 7 clear.
-                v = ds.reshape(ds.shape[0], -1)
-                real = v.abs().amax(dim=1) > s.reshape(s.shape[0], -1).abs().amax(dim=1) * 2.0 ** -20
-                p = f * (mine + 128 * real.to(torch.uint8))
+                # leaves W_sync + D_own a few roundings away from W on rows nobody else changed)
+                # must not win the row over a rank that trained it: such keys carry bit 7 clear.
+                # Per element, against that element's own magnitude (reference_pick restates it)
+                p = f * (mine + 128 * _real_change(ds, s).to(torch.uint8))
                 self.prio.append((p, p.clone()))
                 self.pending.append(self.comm.all_reduce(self.prio[-1][1], op="max",
                                                          async_op=True))
@@ -320,11 +353,12 @@ class DeltaAllReduce(object):
         """Snapshot this rank's delta and launch its asynchronous all-reduce (finishes any
         exchange still pending first).  pick / hot_pick wait for the priority all-reduce first
         (on the device: RCCL's stream, no host block) and zero the rows another rank wins."""
-        if self.world == 1:
+        if not self.active:
             return
         self.prepare()
         self.prepared = False
         self.exchanges += 1
+        self.synced = False
         if self.prio is not None:
             for w in self.pending:
                 w.wait()
@@ -345,7 +379,7 @@ class DeltaAllReduce(object):
     def finish(self):
         """Wait for the pending all-reduce (device-side wait on the current stream) and apply
         the other ranks' deltas."""
-        if self.world == 1 or not self.pending:
+        if not self.active or not self.pending:
             return
         if self.prepared:
             raise RuntimeError("DeltaAllReduce: prepare() without start()")
@@ -373,7 +407,7 @@ class DeltaAllReduce(object):
         """Blocking exchange: afterwards every replica equals W_sync + sum_r D_r, bit for bit
         (nothing trained in between, so W is set to the new W_sync itself rather than to
         W + others' deltas, which differs from it by rounding)."""
-        if self.world == 1:
+        if not self.active:
             return
         self.start()
         self.finish()
@@ -381,9 +415,10 @@ class DeltaAllReduce(object):
 
     def settle(self):
         """After a finish() with nothing trained since its start(): W = W_sync exactly."""
-        if self.world > 1:
+        if self.active:
             for t, s in zip(self.tables, self.snap):
                 t.copy_(s)
+            self.synced = True
 
     @property
     def busy(self):
@@ -402,7 +437,8 @@ class SparseDeltaAllReduce(object):
     Same start / finish / sync protocol; ``last_rows`` / ``last_bytes`` report the previous
     exchange (rows in the union, bytes all-reduced per rank)."""
 
-    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum"):
+    def __init__(self, tables, group=None, bucket_elems=1 << 26, comm=None, combine="sum",
+                 same_start=True, force_exchange=False):
         if combine not in ("sum", "touched_mean"):
             raise ValueError("SparseDeltaAllReduce: combine must be 'sum' or 'touched_mean'")
         self.combine = combine
@@ -410,19 +446,31 @@ class SparseDeltaAllReduce(object):
         self.group = group
         self.comm = comm if comm is not None else TorchComm(group)
         self.world = self.comm.world
+        self.active = self.world > 1 or bool(force_exchange)  # as DeltaAllReduce
         self.bucket = int(bucket_elems)
-        self.snap = [t.clone() for t in self.tables] if self.world > 1 else None
+        if self.active and same_start:  # as DeltaAllReduce: replicas start from rank 0's
+            self._broadcast()
+        self.snap = [t.clone() for t in self.tables] if self.active else None
         self.pending = []
         self.state = []
         self.last_rows = [0] * len(self.tables)
         self.last_bytes = 0
+        self.synced = self.active and same_start
 
-    def reset(self):
-        """As DeltaAllReduce.reset."""
+    def _broadcast(self):
+        for t in self.tables:
+            self.comm.broadcast(t, 0)
+
+    def reset(self, broadcast=None):
+        """As DeltaAllReduce.reset (rank 0's tables taken unless a blocking sync() left the
+        replicas identical)."""
         self.finish()
-        if self.world > 1:
+        if self.active:
+            if broadcast or (broadcast is None and not self.synced):
+                self._broadcast()
             for t, s in zip(self.tables, self.snap):
                 s.copy_(t)
+            self.synced = True
 
     @staticmethod
     def _flags(t, s):
@@ -437,10 +485,11 @@ class SparseDeltaAllReduce(object):
         return (t.view(torch.int32) != s.view(torch.int32)).any(dim=1).to(torch.uint8)
 
     def start(self):
-        if self.world == 1:
+        if not self.active:
             return
         import torch
         self.finish()
+        self.synced = False
         flags = [self._flags(t, s) for t, s in zip(self.tables, self.snap)]
         flat = torch.cat(flags)
         # union over ranks (touched_mean: the number of ranks that changed each row).
@@ -477,7 +526,7 @@ class SparseDeltaAllReduce(object):
             self.last_bytes += n * d * t.element_size()
 
     def finish(self):
-        if self.world == 1 or not self.state:
+        if not self.active or not self.state:
             return
         for w in self.pending:
             w.wait()
@@ -501,7 +550,7 @@ class SparseDeltaAllReduce(object):
 
     def sync(self):
         """Blocking exchange; every replica then equals W_sync bit for bit (as DeltaAllReduce)."""
-        if self.world == 1:
+        if not self.active:
             return
         self.start()
         touched = [st[0] for st in self.state]
@@ -509,6 +558,7 @@ class SparseDeltaAllReduce(object):
         for t, s, idx in zip(self.tables, self.snap, touched):
             if idx.numel():
                 t.index_copy_(0, idx, s.index_select(0, idx))
+        self.synced = True
 
     @property
     def busy(self):
@@ -539,16 +589,20 @@ def reference_touched_mean(w_sync, locals_):
 
 def reference_pick(w_sync, locals_, star):
     """Host restatement of one pick sync for tests: a row changed (bitwise) by some rank takes
-    the delta of the first rank in the order star, star + 1, ... (mod N) that changed it; rows
-    nobody changed stay."""
+    the delta of the first rank in the order star, star + 1, ... (mod N) that changed it by more
+    than rounding (_real_change), else of the first that changed it at all; rows nobody changed
+    stay."""
     s = np.asarray(w_sync, np.float32)
     out = np.array(s, np.float64, copy=True)
     n = len(locals_)
     done = np.zeros(s.shape[0], bool)
-    for j in range(n):
-        w = np.asarray(locals_[(star + j) % n], np.float32)
-        ch = (w.view(np.int32) != s.view(np.int32)).any(axis=1) & ~done
-        out[ch] += w[ch].astype(np.float64) - s[ch].astype(np.float64)
-        done |= ch
+    for real_only in (True, False):
+        for j in range(n):
+            w = np.asarray(locals_[(star + j) % n], np.float32)
+            ch = (w.view(np.int32) != s.view(np.int32)).any(axis=1) & ~done
+            if real_only:
+                ch &= _real_change(w - s, s)
+            out[ch] += w[ch].astype(np.float64) - s[ch].astype(np.float64)
+            done |= ch
     return out
 

@@ -71,7 +71,8 @@ def resp_t_x(resp, X, chunks=256):
     """[K, d] float64: resp^T X (the M-step means numerator, sklearn np.dot(resp.T, X)).  The
     product is K x V x d with V >> K, d: one library GEMM runs it as a skinny GEMM (1.87 ms at C4,
     V = 1M, K = 50, d = 128); split over `chunks` row blocks as a batched GEMM with the partials
-    summed in float64 it takes 0.17-0.22 ms (scripts/sx_probe.py)."""
+    summed in float64 it takes 0.17-0.22 ms (round-2 A/B on one MI355X; DESIGN.md §3.3 prices the
+    whole nk + means step at 0.44 ms)."""
     import torch
     V, K = resp.shape
     d = X.shape[1]

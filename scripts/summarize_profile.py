@@ -59,6 +59,8 @@ def main(src, tag, kernel=KERNEL):
                "raw": pmc}
     if cfg["workload"].startswith("configs[2]/C3"):  # the default bench line reads this one
         json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    if cfg["workload"].startswith("configs[4]/C5"):  # ... and its C5-shard row this one
+        json.dump(traffic, open(os.path.join(dst, "traffic_c5.json"), "w"), indent=1)
     json.dump(traffic, open(os.path.join(dst, "%s_traffic.json" % tag), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 

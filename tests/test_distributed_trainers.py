@@ -11,6 +11,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -152,7 +153,7 @@ def test_trainers_distributed_world2_touched_mean(tmp_path):
         np.testing.assert_array_equal(ld(tab + "0"), ld(tab + "1"))
 
 
-def _worker_seeded(rank, world, port, out_dir, combine):
+def _worker_seeded(rank, world, port, out_dir, combine, sparse=False):
     """Every rank seeds numpy differently (so Model.reset_weights draws different tables)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -162,7 +163,8 @@ def _worker_seeded(rank, world, port, out_dir, combine):
     model, walks, edges = _setup(seed=100 + rank)
     np.save(os.path.join(out_dir, "init%d.npy" % rank), model.node_embedding.numpy().copy())
     Context2Vec(lr=0.1, window_size=2, negative=3, distributed=True, sync_walks=5,
-                combine=combine).train(model, paths=walks, total_nodes=walks.size, alpha=1.0)
+                combine=combine, sparse_sync=sparse).train(model, paths=walks,
+                                                           total_nodes=walks.size, alpha=1.0)
     Node2Vec(lr=0.1, negative=3, distributed=True, combine=combine).train(model, edges=edges,
                                                                         iter=2)
     np.save(os.path.join(out_dir, "node%d.npy" % rank), model.node_embedding.numpy())
@@ -170,12 +172,14 @@ def _worker_seeded(rank, world, port, out_dir, combine):
     dist.destroy_process_group()
 
 
-def test_trainers_distributed_ranks_seeded_differently(tmp_path):
-    """the exchange adds deltas to each rank's own W_sync, so replicas that start apart
-    would never meet.  The exchange takes rank 0's tables when it is built (a broadcast), so ranks
-    seeded differently still leave train() with identical replicas."""
+@pytest.mark.parametrize("sparse", [False, True])
+def test_trainers_distributed_ranks_seeded_differently(tmp_path, sparse):
+    """the exchange adds deltas to each rank's own W_sync, so replicas that start
+    apart would never meet.  The exchange -- dense, or row-sparse (Context2Vec(sparse_sync=True))
+    -- takes rank 0's tables when it is built (a broadcast), so ranks seeded differently still
+    leave train() with identical replicas."""
     world = 2
-    mp.spawn(_worker_seeded, args=(world, _free_port(), str(tmp_path), "touched_mean"),
+    mp.spawn(_worker_seeded, args=(world, _free_port(), str(tmp_path), "touched_mean", sparse),
              nprocs=world, join=True)
     ld = lambda n: np.load(os.path.join(str(tmp_path), n + ".npy"))  # noqa: E731
     assert not np.array_equal(ld("init0"), ld("init1"))   # the ranks did start apart
@@ -199,3 +203,50 @@ def test_trainers_distributed_world2_pick(tmp_path):
         for r in range(world):
             np.testing.assert_allclose(ld("%s%d" % (tab, r)), ref, rtol=0, atol=2e-6)
         np.testing.assert_array_equal(ld(tab + "0"), ld(tab + "1"))
+
+
+def _worker_broadcasts(rank, world, port, out_dir, sparse):
+    """Count the exchange's whole-table broadcasts over three train() calls of one trainer."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from come_amd import distributed as dd
+    from come_amd.context_embeddings import Context2Vec
+    calls = []
+    orig = dd.TorchComm.broadcast
+
+    def counted(self, t, src=0):
+        calls.append(t.numel())
+        return orig(self, t, src)
+    dd.TorchComm.broadcast = counted
+    model, walks, _ = _setup(seed=100 + rank)
+    cl = Context2Vec(lr=0.1, window_size=2, negative=3, distributed=True, sync_walks=5,
+                     sparse_sync=sparse)
+    n = []
+    for _ in range(3):
+        cl.train(model, paths=walks, total_nodes=walks.size, alpha=1.0)
+        n.append(len(calls))
+    ex = cl.exchange(model)          # after a blocking sync: no broadcast
+    n.append(len(calls))
+    ex.start()                       # an exchange in flight: the replicas may differ ...
+    ex.finish()
+    ex.reset()                       # ... so reset() takes rank 0's tables again
+    n.append(len(calls))
+    ex.reset(broadcast=True)
+    n.append(len(calls))
+    np.save(os.path.join(out_dir, "bc%d.npy" % rank), np.array(n))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_exchange_broadcasts_only_when_replicas_may_differ(tmp_path, sparse):
+    """train() ends with a blocking exchange, which leaves the replicas bit-identical,
+    so the next train()'s reset() must not broadcast the whole tables again (41 GB per call at
+    C5's shard).  Broadcasts: 2 tables when the exchange is built, none on later train() calls or
+    a reset() after a blocking sync, 2 after an overlapped exchange or when forced."""
+    world = 2
+    mp.spawn(_worker_broadcasts, args=(world, _free_port(), str(tmp_path), sparse),
+             nprocs=world, join=True)
+    for r in range(world):
+        n = np.load(os.path.join(str(tmp_path), "bc%d.npy" % r)).tolist()
+        assert n == [2, 2, 2, 2, 4, 6], n
