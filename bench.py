@@ -222,7 +222,8 @@ def main():
                          "negative_table)")
     ap.add_argument("--hot-p", type=float, default=None,
                     help="rows holding >= this share of the negative table are updated with "
-                         "float atomics (default training_sdg_inner.DEFAULT_HOT_P; 0 = none)")
+                         "float atomics (default training_sdg_inner.default_hot_share(d); "
+                         "0 = none)")
     ap.add_argument("--opt", action="append", default=[],
                     help="per-call launch option k=v (come_launch_opts field), for A/B runs")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -290,7 +291,7 @@ def main():
     # the rank's shard, each followed by the delta exchange (overlapped with the next launch, the
     # last one blocking)
     opts = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)} or None
-    hot_p = tsi.DEFAULT_HOT_P if args.hot_p is None else args.hot_p
+    hot_p = tsi.default_hot_share(d) if args.hot_p is None else args.hot_p
     learner = Context2Vec(lr=args.lr, window_size=w, negative=n, batch_walks=B,
                           distributed=world > 1, sync_walks=sync_walks,
                           sparse_sync=args.sparse_sync, overlap=not args.no_overlap,

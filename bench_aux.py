@@ -356,7 +356,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hot-p", type=float, default=None,
-                    help="c2: contended-row share (default training_sdg_inner.DEFAULT_HOT_P; "
+                    help="c2: contended-row share (default training_sdg_inner.default_hot_share; "
                          "0 = no float-atomic rows)")
     ap.add_argument("--plain-table", action="store_true",
                     help="c2: draw negatives from the uint32 table instead of the product's "

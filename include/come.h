@@ -65,9 +65,13 @@ enum {
 #define COME_HOT_NONE 0x200
 
 /* Share of the negative table from which a row counts as contended when the library derives the
- * bitmap itself: rows holding >= max(1, floor(COME_DEFAULT_HOT_SHARE * T)) slots
- * (come_amd.training_sdg_inner.DEFAULT_HOT_P; measured in DESIGN.md §3.1). */
+ * bitmap itself: rows holding >= max(1, floor(share * T)) slots, share = COME_DEFAULT_HOT_SHARE
+ * for rows of d <= 128 and COME_DEFAULT_HOT_SHARE_WIDE for wider rows
+ * (come_amd.training_sdg_inner.default_hot_share; measured in DESIGN.md §3.1: with d = 256 and
+ * 10 negatives, plain stores on rows between the two shares lose enough concurrent updates on a
+ * 1M-node power-law graph to move the held-out loss 1.8% below the reference's). */
 #define COME_DEFAULT_HOT_SHARE 5e-6
+#define COME_DEFAULT_HOT_SHARE_WIDE 8e-7
 
 int come_abi_version(void);
 
@@ -322,7 +326,7 @@ int come_set_option(const char *name, int value);
  *           the run computes on its own copy).  The other rows are written back with plain
  *           stores.  Ignored in COME_MODE_SEQUENTIAL.
  *           NULL: the library derives the bitmap from `table` on `stream` before EVERY launch
- *           (rows holding >= COME_DEFAULT_HOT_SHARE of the table: a memset of V counters and a
+ *           (rows holding >= COME_DEFAULT_HOT_SHARE(_WIDE) of the table: a memset of V counters and a
  *           scan of the table, ~0.1 ms at T = 1e8, into library scratch that grows
  *           stream-ordered -- the first call at a larger V allocates, so warm up before capturing
  *           a stream).  Callers that launch many small batches should compute the bitmap once

@@ -74,7 +74,7 @@ class Context2Vec(object):
         self.sparse_sync = bool(sparse_sync)
         self.overlap = bool(overlap)
         self.group = group
-        self.hot_share = hot_share      # None = training_sdg_inner.DEFAULT_HOT_P
+        self.hot_share = hot_share      # None = training_sdg_inner.default_hot_share(d)
         self.launch_opts = launch_opts  # per-call come_launch_opts fields (A/B runs)
         self.combine = combine          # DeltaAllReduce combine rule
         self._exchanges = {}

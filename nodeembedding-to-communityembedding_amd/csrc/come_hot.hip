@@ -106,14 +106,15 @@ static int hot_rows_impl(int dev, const uint32_t *table, uint64_t T, int packed,
     return hip_error(hipGetLastError(), "k_hot_bits launch");
 }
 
-int derive_hot_rows(int dev, const uint32_t *table, uint64_t T, int packed, int64_t V,
+int derive_hot_rows(int dev, const uint32_t *table, uint64_t T, int packed, int64_t V, int d,
                     void *stream, const uint32_t **bits_out) {
     uint32_t *counts = (uint32_t *)stream_scratch(dev, stream, kScratchHotCounts,
                                                   sizeof(uint32_t) * (size_t)V);
     uint32_t *bits = (uint32_t *)stream_scratch(dev, stream, kScratchHotBits,
                                                 sizeof(uint32_t) * (size_t)((V + 31) / 32));
     if (!counts || !bits) return scratch_failed();
-    uint64_t min_count = (uint64_t)(COME_DEFAULT_HOT_SHARE * (double)T);
+    const double share = d <= 128 ? COME_DEFAULT_HOT_SHARE : COME_DEFAULT_HOT_SHARE_WIDE;
+    uint64_t min_count = (uint64_t)(share * (double)T);
     if (min_count < 1) min_count = 1;
     *bits_out = bits;
     return hot_rows_impl(dev, table, T, packed, V, min_count, counts, bits, stream);

@@ -33,9 +33,10 @@ constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchHotCounts = 2, kS
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
 int scratch_failed();
 // The contended-row bitmap a Hogwild launch uses when the caller passes none (come_hot.hip):
-// rows holding >= max(1, floor(COME_DEFAULT_HOT_SHARE * T)) slots of `table` (plain uint32 or, with
+// rows holding >= max(1, floor(share * T)) slots of `table` (share: COME_DEFAULT_HOT_SHARE for rows
+// of d <= 128, COME_DEFAULT_HOT_SHARE_WIDE above) (plain uint32 or, with
 // `packed`, come_pack_table's words), written into library scratch on `stream`.
-int derive_hot_rows(int device, const uint32_t *table, uint64_t T, int packed, int64_t V,
+int derive_hot_rows(int device, const uint32_t *table, uint64_t T, int packed, int64_t V, int d,
                     void *stream, const uint32_t **bits_out);
 // One consistent snapshot of the process-wide launch options (come_set_option; mutex-guarded).
 // Every entry point takes it once at its start, or uses the caller's come_launch_opts (*_ex).

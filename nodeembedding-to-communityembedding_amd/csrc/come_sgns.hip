@@ -142,7 +142,7 @@ extern "C" int come_sgns_o2_ex(float *node, float *ctx, int64_t V, int d, const 
         int dev = 0;
         rc = ensure_init(&dev);
         if (rc) return rc;
-        rc = derive_hot_rows(dev, table, T, packed, V, stream, &hot_rows);
+        rc = derive_hot_rows(dev, table, T, packed, V, d, stream, &hot_rows);
         if (rc) return rc;
     }
     O2Args a{node, ctx, walks, seeds, table, V, P, L, d, window, negative, lr, alpha,
@@ -220,7 +220,7 @@ extern "C" int come_sgns_o1_ex(float *node, int64_t V, int d, const int32_t *edg
         int dev = 0;
         rc = ensure_init(&dev);
         if (rc) return rc;
-        rc = derive_hot_rows(dev, table, T, packed, V, stream, &hot_rows);
+        rc = derive_hot_rows(dev, table, T, packed, V, d, stream, &hot_rows);
         if (rc) return rc;
     }
     // default grid: 8 four-wave workgroups per CU where the run kernel is compiled for 8 waves per

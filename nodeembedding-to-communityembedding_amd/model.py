@@ -145,11 +145,12 @@ class Model(object):
 
     def hot_rows(self, share=None):
         """Bitmap (CUDA) of the contended rows for Hogwild launches: rows holding at least `share`
-        of the negative table (default training_sdg_inner.DEFAULT_HOT_P) -- see come_hot.hip.
+        of the negative table (default training_sdg_inner.default_hot_share(layer1_size)) -- see
+        come_hot.hip.
         Cached per (share, table buffer, V, T) -- rebuilt after build_vocab_ / make_table; None
         when the tables are not on a GPU or share <= 0 (no contended rows)."""
         from . import training_sdg_inner as tsi
-        share = tsi.DEFAULT_HOT_P if share is None else float(share)
+        share = tsi.default_hot_share(self.layer1_size) if share is None else float(share)
         if not getattr(self.table, "is_cuda", False) or share <= 0:
             return None
         cache = self.__dict__.setdefault("_hot_cache", {})

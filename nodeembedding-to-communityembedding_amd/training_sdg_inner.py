@@ -104,10 +104,26 @@ def _opts_arg(opts, update_count=None):
 
 
 # Rows holding at least this share of the negative table are "hot" (contended in Hogwild mode,
-# see come_hot.hip).  Measured (scripts/diag_tierc.py, profiles/r02_ab_hot_threshold.txt): on
-# C3's shape at 100k nodes the held-out loss is 0.81% / 0.11% above the sequential oracle's at
-# shares 1e-5 / 5e-6; at C3 (1M nodes) 5e-6 marks 10k rows and costs no time vs 1e-5.
+# see come_hot.hip): updated by float-atomic deltas, so no concurrent update of theirs is lost.
+# d <= 128 (C2, C3): measured (scripts/diag_tierc.py, profiles/r02_ab_hot_threshold.txt) on C3's
+# shape at 100k nodes the held-out loss is 0.81% / 0.11% above the sequential oracle's at shares
+# 1e-5 / 5e-6; at C3 (1M nodes) 5e-6 marks 10k rows and costs no time vs 1e-5; lower shares cost
+# time there without bringing the bench launch closer to the oracle (1e-6: -0.68% vs -0.80%,
+# +19% time; profiles/r06_hot_share.txt).
+# d > 128 (C5's kernel, d = 256, n = 10): on a 1M-node graph of C5's generator the plain stores of
+# rows between 8e-7 and 5e-6 of the table lose enough concurrent updates (every update of such a
+# row races ~0.1-0.2 others in flight) to train 1.8% BELOW the sequential oracle, outside tier C;
+# 8e-7 lands at -0.40% (+15% launch time on that graph) and leaves C5 itself unchanged (+0.47%
+# -> +0.50%, launch time within 1%); making every row atomic overshoots (+1.5%: stale deltas of
+# thousands of wavefronts summed).  profiles/r06_hot_share.txt.
 DEFAULT_HOT_P = 5e-6
+DEFAULT_HOT_P_WIDE = 8e-7
+
+
+def default_hot_share(d):
+    """The contended-row share the product uses for rows of width d (COME_DEFAULT_HOT_SHARE /
+    _WIDE in come.h)."""
+    return DEFAULT_HOT_P if int(d) <= 128 else DEFAULT_HOT_P_WIDE
 
 
 def hot_rows(table, V, min_count):
@@ -124,7 +140,7 @@ def hot_rows(table, V, min_count):
 
 def _hot_arg(hot, node, V):
     """(pointer, mode flag) for the contended-row argument: "auto" -> NULL (libcome derives the
-    bitmap from the table at DEFAULT_HOT_P), None -> COME_HOT_NONE (every row cold), else a CUDA
+    bitmap from the table at default_hot_share(d)), None -> COME_HOT_NONE (every row cold), else a CUDA
     int32 bitmap of at least ceil(V / 32) words on the tables' device."""
     import torch
     if isinstance(hot, str):
@@ -154,7 +170,7 @@ def sgns_o2(node, ctx, walks, seeds, window, negative, table, lr, alpha=1.0, mod
     options (dict of come_launch_opts fields, see include/come.h); update_count: CUDA int64
     tensor [1] that the launch adds its number of applied target-row updates to; hot: the
     contended-row bitmap of hot_rows() (Hogwild mode: those rows are read per pair and updated
-    with float atomics), "auto" (default: derived from `table` by the library at DEFAULT_HOT_P
+    with float atomics), "auto" (default: derived from `table` by the library at default_hot_share(d)
     before EVERY launch, ~0.1 ms at T = 1e8 -- callers launching many small batches pass
     Model.hot_rows() instead, as the trainers do) or None (no contended rows: every row updated
     with plain stores)."""

@@ -155,12 +155,14 @@ def test_one_wavefront_contended_rows_tier_b(hot_kind):
         assert np.mean(diff <= 1e-5) > 0.95, np.mean(diff <= 1e-5)
 
 
-def test_derived_hot_bitmap_matches_explicit():
+@pytest.mark.parametrize("d", [128, 256])
+def test_derived_hot_bitmap_matches_explicit(d):
     """hot="auto" (the C-ABI's hot_rows == NULL: libcome derives the bitmap, plain or packed
-    table) trains exactly like the explicit come_hot_rows bitmap at DEFAULT_HOT_P, and differs
-    from hot=None (COME_HOT_NONE) -- disjoint walks, so every run is deterministic."""
+    table) trains exactly like the explicit come_hot_rows bitmap at default_hot_share(d) (5e-6 up
+    to d = 128, 8e-7 above), and differs from hot=None (COME_HOT_NONE) -- disjoint walks, so every
+    run is deterministic."""
     rng = np.random.RandomState(9)
-    V, d, L, w, n, T = 1 << 19, 128, 16, 3, 0, 10_000_000  # share 5e-6 = 50 slots: hubs hot
+    V, L, w, n, T = 1 << 19, 16, 3, 0, 10_000_000  # share 5e-6 = 50 slots: hubs hot
     counts = rng.zipf(1.6, V).clip(1, 10 ** 6)
     table = orc.make_table(counts, T)
     node0 = rng.uniform(-1, 1, (V, d)).astype(np.float32)
@@ -169,7 +171,7 @@ def test_derived_hot_bitmap_matches_explicit():
     seeds = rng.randint(0, 2 ** 48, V // L, dtype=np.int64).astype(np.uint64)
     tab = dev(table)
     packed = tsi.pack_table(tab)
-    explicit = tsi.hot_rows(tab, V, max(1, int(tsi.DEFAULT_HOT_P * T)))
+    explicit = tsi.hot_rows(tab, V, max(1, int(tsi.default_hot_share(d) * T)))
     nh = int(np.unpackbits(explicit.cpu().numpy().view(np.uint8)).sum())
     assert 10 < nh < V // 2, nh
     opts = {"o2_kernel": 3}

@@ -376,14 +376,15 @@ def _karate_ranks_worker(rank, world, port, out_dir, seeds):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_karate_nmi_multi_rank_within_reference_range(tmp_path, world):
+def test_karate_nmi_multi_rank_not_below_reference_range(tmp_path, world):
     """The reference's own quality check (adsc_Karate.py:104-148: NMI of the community assignment
     vs karate_zachary.labels) under N-replica training: `world` ranks (processes on one GPU, gloo)
     run the Karate flow with Context2Vec / Node2Vec(distributed=True) and the default exchange;
-    over 10 seeds the mean NMI is no lower than the bottom of the reference's seed range
-    0.48-0.73 -- the averaged exchange lands inside it at 2 ranks and just above it
-    at 4 (0.75, r05e: the replicas' mean carries less SGD noise) -- and the replicas
-    agree (every rank computes the same assignments)."""
+    asserted: over 10 seeds the mean NMI is NOT BELOW the bottom of the reference's seed range
+    0.48-0.73, and the replicas agree (every rank computes the same assignments).
+    Not asserted: that it stays inside the range -- it does at 2 ranks (mean 0.683) but lands
+    ABOVE it at 4 (0.745, r05e: the replicas' mean carries less SGD noise than the reference's
+    Hogwild), which is why distributed training is documented as non-parity."""
     import socket
     import torch.multiprocessing as mp
     sk = socket.socket()
@@ -397,7 +398,7 @@ def test_karate_nmi_multi_rank_within_reference_range(tmp_path, world):
     for r in range(1, world):
         np.testing.assert_array_equal(nmi[r], nmi[0])
     print("Karate NMI, %d ranks: %s mean %.3f" % (world, np.round(nmi[0], 3), nmi[0].mean()))
-    assert 0.48 <= nmi[0].mean() <= 1.0, nmi[0]
+    assert nmi[0].mean() >= 0.48, nmi[0]
 
 
 # ---- configs[4]/C5 (d = 256, n = 10) -----------------------------------------------------------
@@ -411,7 +412,8 @@ def c5_launch_losses(x, fx, runs=2):
     ri, rp, rn = x.heldout(w, n)
     l0 = None
     tab = dev(x.table)
-    hot = tsi.hot_rows(tab, x.g.V, int(tsi.DEFAULT_HOT_P * len(x.table)))
+    # the product's contended rows for this row width (Model.hot_rows: default_hot_share(d))
+    hot = tsi.hot_rows(tab, x.g.V, int(tsi.default_hot_share(x.node0.shape[1]) * len(x.table)))
     packed = tsi.pack_table(tab)
     assert packed is not None
     walks, seeds = dev(x.train), dev(x.seeds)
@@ -451,19 +453,20 @@ def test_o2_hogwild_c5():
     assert max(abs(r) for r in rel) < 0.01, rel  # SURVEY.md §8c tier C
 
 
-def test_o2_hogwild_c5_kernel_on_1m_nodes_regression():
-    """The same kernel on a 1M-node graph of C5's generator, where hubs hold 10x the table share
-    they hold at C5's 10M nodes (the top row 5.0e-4 vs 1.6e-4; rows >= 5e-6 of the table: 9.9% vs
-    1.0% of it).  NOT a tier-C pass: the GPU launch (4,096 wavefronts in flight) trains to a LOWER
-    held-out loss than the sequential oracle, -1.8% (the reference's CPU Hogwild, 7 threads:
-    +0.09%); it shrinks with fewer wavefronts in flight (max_waves 2048 / 1024 / 512: -1.3 / -0.9 /
-    -0.4%, profiles/r04_c5_1m_waves.json) -- stale reads of hub rows under thousands of
-    concurrent updaters.  Guarded here against regressions: within -2.5% .. +1%."""
+def test_o2_hogwild_c5_kernel_on_1m_nodes():
+    """Tier C for C5's kernel on a 1M-node graph of C5's generator, where rows hold 10x the table
+    share they hold at C5's 10M nodes (the top row 5.0e-4 vs 1.6e-4): held-out loss of two product
+    launches within 1% of the sequential oracle's (tests/golden/tierc_c5_1m_seq.json).  Until
+    round 5 this failed at -1.8% (the test then only guarded -2.5% .. +1%): rows between 8e-7 and
+    5e-6 of the table were written with plain stores, and on this graph each of their updates races
+    0.1-0.2 others in flight, so enough updates were lost to damp the SGD noise below the
+    reference's.  The product now makes them contended rows at d > 128 (default_hot_share:
+    -0.40%, profiles/r06_hot_share.txt)."""
     import json
     from tierc_inputs import c5_1m_inputs
     fx = json.load(open(os.path.join(GOLDEN, "tierc_c5_1m_seq.json")))
     rel = c5_launch_losses(c5_1m_inputs(), fx)
-    assert all(-0.025 < r < 0.01 for r in rel), rel
+    assert max(abs(r) for r in rel) < 0.01, rel  # SURVEY.md §8c tier C
 
 
 # ---- the multi-GPU path: N ranks' delta-sum training (SURVEY.md §8e) --------------------------
@@ -539,11 +542,19 @@ def test_o2_multi_rank_exchange_regression_band(c3_1m, world):
         (loss, fx["seq_loss"])
 
 
-def test_o2_default_period_over_4m_walks():
+# ranks -> (exchanges per rank, band) at the default period over the 4M-walk fixture: 2 ranks make
+# 4 exchanges (measured -12.4%, r05); 8 ranks -- the C5 topology -- make ONE (their whole shard is
+# one period; measured -19.4% in round 3, profiles/r04_tierc_replicas_c3_4m.json), a band of its own
+# around that (the trainers' default period at 8 ranks had no quality test).
+DEFAULT_PERIOD_CASES = {2: (4, TOUCHED_MEAN_BAND), 8: (1, (-0.25, -0.12))}
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_o2_default_period_over_4m_walks(world):
     """The multi-GPU default period (context_embeddings.DEFAULT_SYNC_WALKS = 524,288 walks per rank
     between exchanges, overlapped, touched_mean) over the 4,194,304 walks of the C3_4M fixture
-    (tests/golden/tierc_c3_4m_seq.json: the sequential oracle, ~3 h of one core) on 2 ranks: 4
-    exchanges per rank.  In the same band as at 1M walks (measured -12.4%, r04)."""
+    (tests/golden/tierc_c3_4m_seq.json: the sequential oracle, ~3 h of one core) on 2 ranks (4
+    exchanges per rank, the 1M-walk band) and 8 ranks (1 exchange: DEFAULT_PERIOD_CASES)."""
     import json
     from come_amd.context_embeddings import DEFAULT_SYNC_WALKS
     from replica_sim import train_replicas
@@ -555,17 +566,18 @@ def test_o2_default_period_over_4m_walks():
     tab = dev(x.table)
     hot = tsi.hot_rows(tab, x.g.V, int(tsi.DEFAULT_HOT_P * len(x.table)))
     st = {}
-    node, ctx = train_replicas(x.node0, np.zeros_like(x.node0), x.train, x.seeds, 2,
+    node, ctx = train_replicas(x.node0, np.zeros_like(x.node0), x.train, x.seeds, world,
                                DEFAULT_SYNC_WALKS, 5, 5, tsi.pack_table(tab), hot, 0.1, stats=st)
     loss = sgns_loss(node.cpu().numpy(), ctx.cpu().numpy(), ri, rp, rn)
     del node, ctx
     torch.cuda.empty_cache()
     rel = (loss - fx["seq_loss"]) / fx["seq_loss"]
-    print("C3 4M walks, 2 ranks x %d walks per exchange, %d exchanges: held-out loss %.5f vs seq "
-          "%.5f (rel %+.5f)" % (DEFAULT_SYNC_WALKS, st["exchanges"], loss, fx["seq_loss"], rel))
-    assert st["exchanges"] == 4
-    assert np.isfinite(loss) and TOUCHED_MEAN_BAND[0] < rel < TOUCHED_MEAN_BAND[1], \
-        (loss, fx["seq_loss"])
+    print("C3 4M walks, %d ranks x %d walks per exchange, %d exchanges: held-out loss %.5f vs seq "
+          "%.5f (rel %+.5f)" % (world, DEFAULT_SYNC_WALKS, st["exchanges"], loss, fx["seq_loss"],
+                                rel))
+    exchanges, band = DEFAULT_PERIOD_CASES[world]
+    assert st["exchanges"] == exchanges
+    assert np.isfinite(loss) and band[0] < rel < band[1], (loss, fx["seq_loss"])
 
 
 @pytest.fixture(scope="module")
