@@ -293,3 +293,34 @@ def test_pick_real_change_beats_rounding_level_change():
     assert torch.equal(tabs[0][4], torch.nextafter(base[4], base[4] + 1.0))  # still taken
     for t in tabs[1:]:
         assert torch.equal(t, tabs[0])
+
+
+def test_pick_real_change_on_a_large_norm_row():
+    """the rounding-level rule is per element.  A real late-training update that moves
+    only the row's small elements (here by 1e-4 on elements of magnitude 1e-3) while its largest
+    element is 1e3 -- below 2^-20 of the row's largest |W_sync|, the round-4 row-max rule -- is a
+    real change and wins the row against a rank whose change is one ulp; reference_pick agrees."""
+    from come_amd.distributed import LocalReplicas, reference_pick, _real_change
+    W, V, d = 2, 3, 8
+    g = LocalReplicas(W)
+    base = torch.full((V, d), 1e-3)
+    base[:, 0] = 1e3
+    tabs = [base.clone() for _ in range(W)]
+    exs = [DeltaAllReduce([tabs[r]], comm=g.comm(r), combine="pick") for r in range(W)]
+    w_sync = base.numpy().copy()
+    tabs[0][1] = torch.nextafter(tabs[0][1], tabs[0][1] + 1.0)  # rank 0 (the star): one ulp
+    tabs[1][1, 1:] += 1e-4                                      # rank 1: a real, small update
+    assert (tabs[1][1] - base[1]).abs().max() < base[1].abs().max() * 2.0 ** -20
+    assert _real_change((tabs[1] - base).numpy(), w_sync)[1]
+    assert not _real_change((tabs[0] - base).numpy(), w_sync)[1]
+    locs = [t.numpy().copy() for t in tabs]
+    for e in exs:
+        e.prepare()
+    for e in exs:
+        e.start()
+    for e in exs:
+        e.finish()
+        e.settle()
+    np.testing.assert_array_equal(tabs[0][1].numpy(), locs[1][1])   # rank 1's delta won
+    np.testing.assert_allclose(tabs[0].numpy(), reference_pick(w_sync, locs, 0), rtol=0, atol=0)
+    assert torch.equal(tabs[1], tabs[0])

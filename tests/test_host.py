@@ -254,3 +254,17 @@ def test_scatter_chunks_fill_whole_rounds(V, K, d):
             assert (groups * c) % 512 > 512 - groups or (groups * c) % 512 == 0
     if (V, K, d) == (1_000_000, 50, 128):
         assert c == 163  # = the measured C4 grid (7.96 rounds, profiles/r05_ab_gmm_diag.txt)
+
+
+def test_default_hot_share_by_row_width():
+    """The contended-row share the product uses (training_sdg_inner.default_hot_share) is the
+    one the library derives the bitmap with (come.h COME_DEFAULT_HOT_SHARE / _WIDE): 5e-6 up to
+    d = 128, 8e-7 above (profiles/r06_hot_share.txt)."""
+    import re
+    import come_amd.training_sdg_inner as tsi
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "come.h")).read()
+    narrow = float(re.search(r"#define COME_DEFAULT_HOT_SHARE\s+(\S+)", hdr).group(1))
+    wide = float(re.search(r"#define COME_DEFAULT_HOT_SHARE_WIDE\s+(\S+)", hdr).group(1))
+    assert [tsi.default_hot_share(d) for d in (2, 64, 128)] == [narrow] * 3 == [5e-6] * 3
+    assert [tsi.default_hot_share(d) for d in (129, 256, 512)] == [wide] * 3 == [8e-7] * 3
