@@ -125,6 +125,43 @@ def secondary_rows(timeout_s=150):
     return out
 
 
+def c5_multi_gpu_row(args, rank, world, timeout_s=600):
+    """configs[4]/C5 at this job's N GPUs (BASELINE: 10M nodes / 100M edges, d = 256, n = 10,
+    8 x MI355X): every rank starts this script as a child on the 10M-node graph -- its own
+    process group (same RANK / WORLD_SIZE, MASTER_PORT + 1), the product's distributed trainer,
+    1M walks per rank per step, the dense overlapped exchange of both 10.24 GB tables -- after
+    the C3 timed region.  Outside `value`; rank 0 returns the child's line as a row (an error
+    string if it failed or timed out), the other ranks None."""
+    import subprocess
+    env = dict(os.environ)
+    env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 1)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--nodes",
+           str(args.c5_nodes), "--dim", "256", "--negative", "10", "--steps", "3", "--warmup", "1",
+           "--no-secondary", "--no-cpu-baseline", "--dist-backend", args.dist_backend,
+           "--traffic-json", os.path.join(ROOT, "profiles", "traffic_c5.json")]
+    if args.all_ranks_device0:
+        cmd.append("--all-ranks-device0")
+    t0 = time.time()
+    try:
+        # stdout carries the child's JSON line; its stderr (progress) passes through
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return "error: timed out after %ds" % timeout_s if rank == 0 else None
+    if rank != 0:
+        return None
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not line:
+        return "error rc=%d (the child's stderr is in this job's log)" % r.returncode
+    j = json.loads(line[-1])
+    rf = j["roofline"]
+    return {"metric": j["metric"], "value": j["value"], "unit": j["unit"], "n_gpus": j["n_gpus"],
+            "ms_per_step": j["ms_per_step"], "workload": j["config"]["workload"],
+            "parallelism": j["config"]["parallelism"], "scaling": j["scaling"],
+            "roofline_frac": rf["frac_skip_adjusted"],
+            "roofline_frac_all_targets_written": rf["frac"],
+            "avg_kernel_ms": rf["avg_kernel_ms"], "wall_s": time.time() - t0}
+
+
 def calibration_ratio():
     try:
         c = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))
@@ -205,7 +242,11 @@ def main():
                     help="0 = every CPU this process may use (affinity and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="N=1: skip the secondary rows (C2 / C4 / walker via bench_aux.py)")
+                    help="skip the secondary rows (N=1: C2 / C4 / walker via bench_aux.py and one "
+                         "GPU's share of C5; N>1: C5 on the job's N GPUs)")
+    ap.add_argument("--c5-nodes", type=int, default=10_000_000,
+                    help="N>1: nodes of the C5 secondary row's graph (configs[4]: 10M; smaller "
+                         "only to rehearse the multi-process plumbing, e.g. over gloo on one GPU)")
     ap.add_argument("--combine", default="touched_mean",
                     help="N>1: delta exchange combine rule (DeltaAllReduce; DESIGN.md §6)")
     ap.add_argument("--sparse-sync", action="store_true",
@@ -315,11 +356,15 @@ def main():
     stream = torch.cuda.current_stream(dev)
     for s in range(args.warmup):
         step(s)
+        if rank == 0:
+            log("warm-up step %d of %d enqueued" % (s + 1, args.warmup))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
+    if rank == 0:
+        log("warm-up done (%d steps); timing %d steps" % (args.warmup, args.steps))
     ev = []
     t_start = time.perf_counter()
     for k in range(args.steps):
@@ -345,6 +390,9 @@ def main():
     assert torch.isfinite(model.node_embedding).all() and torch.isfinite(
         model.context_embedding).all(), "non-finite embedding after training"
 
+    c5_multi = None
+    if world > 1 and not args.no_secondary:
+        c5_multi = c5_multi_gpu_row(args, rank, world)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -402,7 +450,7 @@ def main():
                              "AVX2+FMA" if isa else "baseline-ISA", threads, cw, cp, cel,
                              rthreads, "%.3f" % ratio if ratio else "n/a")}
 
-    secondary = None
+    secondary = {"c5": c5_multi} if c5_multi is not None else None
     if world == 1 and not args.no_secondary:
         log("secondary rows (bench_aux.py c2 / c4 / walks, bench.py C5 shard; outside the timed region)")
         secondary = secondary_rows()
