@@ -135,6 +135,9 @@ def c5_multi_gpu_row(args, rank, world, timeout_s=600):
     import subprocess
     env = dict(os.environ)
     env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 1)
+    # torch.distributed.run tells its workers to join the agent's store on MASTER_PORT; the
+    # children's group has no agent, so rank 0's child hosts its own store on MASTER_PORT + 1
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--nodes",
            str(args.c5_nodes), "--dim", "256", "--negative", "10", "--steps", "3", "--warmup", "1",
            "--no-secondary", "--no-cpu-baseline", "--dist-backend", args.dist_backend,
