@@ -482,7 +482,8 @@ def main():
             "workload": "%s: O2 SGNS over random walks, power-law %d nodes / %d "
                         "edges, d=%d, negative=%d, window=%d, walk_length=%d, table_size=%d, lr=%g, "
                         "alpha=1" % (
-                            "configs[4]/C5 (one GPU's shard)" if d == 256 and n == 10
+                            ("configs[4]/C5 (one GPU's shard)" if world == 1
+                             else "configs[4]/C5 on %d GPUs" % world) if d == 256 and n == 10
                             else "configs[2]/C3", V, g.num_edges, d, n, w, L, args.table_size,
                             args.lr),
             "walks_per_step_per_gpu": B,

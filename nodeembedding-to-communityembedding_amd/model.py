@@ -111,7 +111,14 @@ class Model(object):
         import torch
         dev = self._torch_device()
         V, d, K = self.vocab_size, self.layer1_size, self.k
-        node = np.random.uniform(low=-1, high=1, size=(V, d)).astype(np.float32)  # model.py:86
+        # = np.random.uniform(low=-1, high=1, size=(V, d)).astype(np.float32) (model.py:86): the
+        # same draws from the global stream, taken in row blocks so that no V x d float64
+        # temporary exists (20 GB at C5's 10M x 256, per rank)
+        node = np.empty((V, d), np.float32)
+        step = max(1, (1 << 22) // max(1, d))
+        for r0 in range(0, V, step):
+            r1 = min(V, r0 + step)
+            node[r0:r1] = np.random.uniform(low=-1, high=1, size=(r1 - r0, d))
         self.node_embedding = torch.from_numpy(node).to(dev)
         self.context_embedding = torch.zeros((V, d), dtype=torch.float32, device=dev)
         self.centroid = torch.zeros((K, d), dtype=torch.float32, device=dev)
