@@ -125,7 +125,7 @@ def secondary_rows(timeout_s=150):
     return out
 
 
-def c5_multi_gpu_row(args, rank, world, timeout_s=600):
+def c5_multi_gpu_row(args, rank, world, timeout_s=240):
     """configs[4]/C5 at this job's N GPUs (BASELINE: 10M nodes / 100M edges, d = 256, n = 10,
     8 x MI355X): every rank starts this script as a child on the 10M-node graph -- its own
     process group (same RANK / WORLD_SIZE, MASTER_PORT + 1), the product's distributed trainer,
