@@ -196,6 +196,14 @@ int come_pyrandom_seed(uint64_t seed, uint32_t *state625);
  * random(), kind 1 = _randbelow(arg) (arg <= 2^32).  Test hook for the restated stream. */
 int come_pyrandom_draw(uint32_t *state625, int kind, uint64_t arg, int64_t count, double *out);
 
+/* Host: the per-walk / per-edge seeds train_o2 / train_o1 draw from the GLOBAL numpy RNG
+ * (pyx:477 / pyx:427: next_random = 2^24 * randint(0, 2^24) + randint(0, 2^24), two draws per
+ * call, in call order), for n consecutive calls at once.  state625 = the 624 MT19937 words and
+ * the position of numpy.random.get_state() (legacy RandomState: each bounded randint below 2^32
+ * consumes one 32-bit output, masked to 24 bits -- the mask equals the range, so nothing is ever
+ * rejected), advanced in place (set_state() it back).  out: uint64 [n]. */
+int come_np_draw_seeds(uint32_t *state625, int64_t n, uint64_t *out);
+
 /* Host: nx.Graph().add_edges_from(edges) (graph_utils.py:60-69) in networkx order.
  * edges int64 [E x 2] node ids in file order.  Outputs (capacities 2E, 2E+1 for rowptr):
  * node_ids[V] = list(G.nodes()) (first appearance), rowptr/col = adjacency in insertion order

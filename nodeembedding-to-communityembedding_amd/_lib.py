@@ -22,7 +22,8 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_fast_version", "come_sgns_o2", "come_sgns_o1", "come_community_grad",
            "come_gmm_resp", "come_make_table", "come_count_o2_pairs", "come_set_option",
            "come_random_walks", "come_walks_reference", "come_pyrandom_seed",
-           "come_pyrandom_draw", "come_graph_from_edges", "come_read_int_rows",
+           "come_pyrandom_draw", "come_np_draw_seeds", "come_graph_from_edges",
+           "come_read_int_rows",
            "come_write_int_rows", "come_save_embedding", "come_format_f32",
            "come_gmm_estep", "come_gmm_scatter", "come_pack_table",
            "come_delta_begin", "come_delta_end", "come_get_options", "come_sgns_o2_ex",
@@ -125,6 +126,7 @@ def lib():
     L.come_walks_reference.argtypes = [P, P, i64, i32, P, P, i32, f64, P, i32, P]
     L.come_pyrandom_seed.argtypes = [u64, P]
     L.come_pyrandom_draw.argtypes = [P, i32, u64, i64, P]
+    L.come_np_draw_seeds.argtypes = [P, i64, P]
     L.come_graph_from_edges.argtypes = [P, i64, P, P, P, P, P, P, P]
     L.come_read_int_rows.argtypes = [cp, P, i64, i32, P, P]
     L.come_write_int_rows.argtypes = [cp, P, i64, i32, i32]

@@ -293,6 +293,20 @@ extern "C" int come_pyrandom_draw(uint32_t *state625, int kind, uint64_t arg, in
     return COME_OK;
 }
 
+extern "C" int come_np_draw_seeds(uint32_t *state625, int64_t n, uint64_t *out) {
+    if (!state625 || (!out && n > 0)) return set_error(COME_E_INVALID, "null pointer");
+    if (n < 0) return set_error(COME_E_INVALID, "n must be >= 0");
+    PyRandom r;  // CPython's MT19937 core is numpy's legacy one (genrand_int32, same state)
+    if (!r.set(state625)) return set_error(COME_E_INVALID, "bad MT19937 state position");
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t a = r.genrand() & 0xFFFFFFu;  // randint(0, 2^24): masked, never rejected
+        const uint64_t b = r.genrand() & 0xFFFFFFu;
+        out[i] = (a << 24) + b;
+    }
+    r.get(state625);
+    return COME_OK;
+}
+
 extern "C" int come_graph_from_edges(const int64_t *edges, int64_t E, int64_t *node_ids,
                                      int64_t *V_out, int64_t *rowptr, int32_t *col,
                                      int64_t *degree, int32_t *edge_pos, int64_t *E_out) {

@@ -43,12 +43,25 @@ def exp_table():
 
 def draw_seeds(n):
     """Initial next_random of n consecutive train_o1/train_o2 calls, drawn from the global numpy
-    RNG exactly as pyx:427/477 does per call: 2^24 * randint(0, 2^24) + randint(0, 2^24)."""
+    RNG exactly as pyx:427/477 does per call: 2^24 * randint(0, 2^24) + randint(0, 2^24).
+    The stream is generated natively (come_np_draw_seeds: numpy's legacy MT19937, ~10 ms per 1M
+    calls instead of numpy's 56 ms -- the host cost of every O1 pass and O2 batch) from
+    np.random.get_state(), and the global state is advanced with set_state() exactly as numpy's
+    own 2n randint draws would leave it (tests/test_host.py)."""
     n = int(n)
     if n == 0:
         return np.zeros(0, np.uint64)
-    ab = np.random.randint(0, 2 ** 24, size=2 * n).astype(np.uint64)
-    return (ab[0::2] << np.uint64(24)) + ab[1::2]
+    st = np.random.get_state()
+    if st[0] != "MT19937":  # pragma: no cover (the legacy global RNG is always MT19937)
+        ab = np.random.randint(0, 2 ** 24, size=2 * n).astype(np.uint64)
+        return (ab[0::2] << np.uint64(24)) + ab[1::2]
+    state = np.empty(625, np.uint32)
+    state[:624] = st[1]
+    state[624] = st[2]
+    out = np.empty(n, np.uint64)
+    check(_lib.lib().come_np_draw_seeds(ptr(state), n, ptr(out)), "come_np_draw_seeds")
+    np.random.set_state((st[0], state[:624].copy(), int(state[624]), st[3], st[4]))
+    return out
 
 
 def _require_cuda(t, name, dtype):

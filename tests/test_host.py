@@ -268,3 +268,28 @@ def test_default_hot_share_by_row_width():
     wide = float(re.search(r"#define COME_DEFAULT_HOT_SHARE_WIDE\s+(\S+)", hdr).group(1))
     assert [tsi.default_hot_share(d) for d in (2, 64, 128)] == [narrow] * 3 == [5e-6] * 3
     assert [tsi.default_hot_share(d) for d in (129, 256, 512)] == [wide] * 3 == [8e-7] * 3
+
+
+@pytest.mark.parametrize("seed", [0, 1234, 2 ** 31 + 7])
+def test_draw_seeds_is_numpy_stream(seed):
+    """draw_seeds (native come_np_draw_seeds) == the reference's per-call seeding, pyx:427/477
+    (2^24 * randint(0, 2^24) + randint(0, 2^24) from the GLOBAL numpy RNG, call after call): the
+    same values and the global RNG left exactly where numpy's own draws leave it, across the
+    624-word regeneration boundary and with a cached Gaussian pending."""
+    def reference(n):
+        out = np.empty(n, np.uint64)
+        for i in range(n):  # the reference's per-call expression, pyx:477
+            out[i] = (2 ** 24) * np.random.randint(0, 2 ** 24) + np.random.randint(0, 2 ** 24)
+        return out
+    for n in (0, 1, 311, 312, 313, 2000):
+        np.random.seed(seed)
+        np.random.random(5)
+        np.random.standard_normal()  # leaves a cached Gaussian in the legacy state
+        got, after = tsi.draw_seeds(n), np.random.random(4)
+        gauss = np.random.standard_normal()
+        np.random.seed(seed)
+        np.random.random(5)
+        np.random.standard_normal()
+        want, after_ref = reference(n), np.random.random(4)
+        assert np.array_equal(got, want), n
+        assert np.array_equal(after, after_ref) and gauss == np.random.standard_normal(), n
