@@ -22,6 +22,36 @@ import numpy as np
 from . import training_sdg_inner as tsi
 
 
+class _SeedUpload(object):
+    """Every edge's seed for one pass (training_sdg_inner.draw_seeds: the global numpy RNG, pyx:427)
+    drawn straight into one of two pinned host buffers and copied to the device asynchronously, so
+    the host draws pass p + 1's seeds while pass p trains (a pageable copy would wait for the
+    launch before it).  A buffer is rewritten only after its previous copy has completed."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.bufs = [None, None]
+        self.events = [None, None]
+        self.k = 0
+
+    def __call__(self, n):
+        import torch
+        if self.dev.type != "cuda":
+            return torch.from_numpy(tsi.draw_seeds(n).view(np.int64))
+        i = self.k % 2
+        self.k += 1
+        if self.bufs[i] is None or self.bufs[i].numel() != n:
+            self.bufs[i] = torch.empty(n, dtype=torch.int64, pin_memory=True)
+            self.events[i] = None
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        tsi.draw_seeds(n, out=self.bufs[i].numpy().view(np.uint64))
+        d = self.bufs[i].to(self.dev, non_blocking=True)
+        self.events[i] = torch.cuda.Event()
+        self.events[i].record(torch.cuda.current_stream(self.dev))
+        return d
+
+
 class Node2Vec(object):
     def __init__(self, lr=0.2, workers=1, negative=0, deterministic=False, distributed=False,
                  sync_edges=None, group=None, combine="touched_mean"):
@@ -89,14 +119,18 @@ class Node2Vec(object):
         rank, world = world_of(self.group) if self.distributed else (0, 1)
         ex = self.exchange(model) if world > 1 else None
         pairs = 0
+        n_valid = None
+        seeds_to = _SeedUpload(dev)
         for it in range(int(iter)):
             if it > 0 and model.down_sampling:  # every pass draws its own sample (:47)
                 rows = self._edge_rows(model, edges)
                 ed = torch.from_numpy(rows).to(dev)
-            seeds = tsi.draw_seeds(rows.shape[0])
+                n_valid = None
             lo, hi = shard_range(rows.shape[0], rank, world)
-            pairs += 2 * int((rows[lo:hi] >= 0).all(axis=1).sum())
-            sd = torch.from_numpy(seeds.view(np.int64)).to(dev)
+            if n_valid is None:
+                n_valid = 2 * int((rows[lo:hi] >= 0).all(axis=1).sum())
+            pairs += n_valid
+            sd = seeds_to(rows.shape[0])
             if ex is None:
                 tsi.sgns_o1(model.node_embedding, ed, sd, self.negative, model.negative_table(),
                             self.lr, mode, hot=hot)

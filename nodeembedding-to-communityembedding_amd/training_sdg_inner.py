@@ -41,7 +41,7 @@ def exp_table():
     return out
 
 
-def draw_seeds(n):
+def draw_seeds(n, out=None):
     """Initial next_random of n consecutive train_o1/train_o2 calls, drawn from the global numpy
     RNG exactly as pyx:427/477 does per call: 2^24 * randint(0, 2^24) + randint(0, 2^24).
     The stream is generated natively (come_np_draw_seeds: numpy's legacy MT19937, ~10 ms per 1M
@@ -51,6 +51,9 @@ def draw_seeds(n):
     n = int(n)
     if n == 0:
         return np.zeros(0, np.uint64)
+    if out is not None and (out.dtype != np.uint64 or out.shape != (n,) or
+                            not out.flags["C_CONTIGUOUS"]):
+        raise ValueError("out must be a contiguous uint64 array of %d seeds" % n)
     st = np.random.get_state()
     if st[0] != "MT19937":  # pragma: no cover (the legacy global RNG is always MT19937)
         ab = np.random.randint(0, 2 ** 24, size=2 * n).astype(np.uint64)
@@ -58,7 +61,7 @@ def draw_seeds(n):
     state = np.empty(625, np.uint32)
     state[:624] = st[1]
     state[624] = st[2]
-    out = np.empty(n, np.uint64)
+    out = np.empty(n, np.uint64) if out is None else out
     check(_lib.lib().come_np_draw_seeds(ptr(state), n, ptr(out)), "come_np_draw_seeds")
     np.random.set_state((st[0], state[:624].copy(), int(state[624]), st[3], st[4]))
     return out
