@@ -119,6 +119,30 @@ struct PyRandom {
             if (r < n) return r;
         }
     }
+    // Whole blocks at once (come_np_draw_seeds): regenerate the 624 words in place and temper
+    // all of them -- branch-free loops the compiler vectorises (genrand() above costs ~1.4 ns
+    // per output with its per-call branch; this ~0.4 ns).  Same recurrence, same outputs.
+    void regenerate() {
+        int kk;
+        for (kk = 0; kk < N - M; kk++) {  // reads mt[kk + 1], mt[kk + M]: not yet rewritten
+            const uint32_t y = (mt[kk] & 0x80000000U) | (mt[kk + 1] & 0x7fffffffU);
+            mt[kk] = mt[kk + M] ^ (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
+        }
+        for (; kk < N - 1; kk++) {  // reads mt[kk + M - N]: rewritten 227 words earlier
+            const uint32_t y = (mt[kk] & 0x80000000U) | (mt[kk + 1] & 0x7fffffffU);
+            mt[kk] = mt[kk + (M - N)] ^ (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
+        }
+        const uint32_t y = (mt[N - 1] & 0x80000000U) | (mt[0] & 0x7fffffffU);
+        mt[N - 1] = mt[M - 1] ^ (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
+        mti = 0;
+    }
+    static uint32_t temper(uint32_t y) {
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680U;
+        y ^= (y << 15) & 0xefc60000U;
+        y ^= (y >> 18);
+        return y;
+    }
     void get(uint32_t *st) const {
         memcpy(st, mt, sizeof(mt));
         st[N] = (uint32_t)mti;
@@ -298,10 +322,29 @@ extern "C" int come_np_draw_seeds(uint32_t *state625, int64_t n, uint64_t *out) 
     if (n < 0) return set_error(COME_E_INVALID, "n must be >= 0");
     PyRandom r;  // CPython's MT19937 core is numpy's legacy one (genrand_int32, same state)
     if (!r.set(state625)) return set_error(COME_E_INVALID, "bad MT19937 state position");
-    for (int64_t i = 0; i < n; ++i) {
-        const uint64_t a = r.genrand() & 0xFFFFFFu;  // randint(0, 2^24): masked, never rejected
-        const uint64_t b = r.genrand() & 0xFFFFFFu;
-        out[i] = (a << 24) + b;
+    // 2n consecutive outputs (randint(0, 2^24) each: one output masked, never rejected), block
+    // by block: out[i] = 2^24 * t[2i] + t[2i + 1]
+    uint32_t t[PyRandom::N + 1];
+    int64_t need = 2 * n, done = 0;
+    uint64_t hi = 0;
+    bool have_hi = false;
+    while (need > 0) {
+        if (r.mti >= PyRandom::N) r.regenerate();
+        const int take = (int)std::min<int64_t>(need, PyRandom::N - r.mti);
+        for (int k = 0; k < take; ++k) t[k] = PyRandom::temper(r.mt[r.mti + k]) & 0xFFFFFFu;
+        r.mti += take;
+        need -= take;
+        int k = 0;
+        if (have_hi) {  // the high half drawn at the end of the previous block
+            out[done++] = (hi << 24) + t[0];
+            have_hi = false;
+            k = 1;
+        }
+        for (; k + 1 < take; k += 2) out[done++] = ((uint64_t)t[k] << 24) + t[k + 1];
+        if (k < take) {
+            hi = t[k];
+            have_hi = true;
+        }
     }
     r.get(state625);
     return COME_OK;
