@@ -85,12 +85,26 @@ def walks_to_rows(model, paths, max_len=None):
     Down-sampling (model.down_sampling > 0) draws one np.random.random_sample per in-vocabulary
     node whose sample_probability < 1, walk by walk, node by node.
     A CUDA tensor of node ids (e.g. come_amd.graph_utils.device_walks output mapped to ids, -1
-    after a walk's end) is converted on the device and returned as a CUDA int32 tensor."""
+    after a walk's end) is converted on the device and returned as a CUDA int32 tensor; so is a
+    host 2-D id array when the model's tables are on the GPU (uploaded, then mapped there), unless
+    it needs the host path (OOV ids inside a walk, down-sampling)."""
     if hasattr(paths, "is_cuda") and paths.is_cuda:
         rows = _device_rows(model, paths, max_len)
         if rows is not None:
             return rows
         paths = paths.cpu().numpy()
+    if (isinstance(paths, np.ndarray) and paths.ndim == 2 and paths.size and
+            not model.down_sampling and paths.dtype.kind in "iu" and
+            getattr(getattr(model, "node_embedding", None), "is_cuda", False)):
+        # a host id array for a model on the GPU: upload the ids and map them there (1M walks x
+        # 80: ~0.1 s instead of 1.3 s of numpy on the host, beside a 0.8 s launch); the host path
+        # below remains for OOV ids inside a walk and for down-sampling
+        import torch
+        ids = paths if paths.dtype in (np.int32, np.int64) else paths.astype(np.int64)
+        rows = _device_rows(model, torch.from_numpy(np.ascontiguousarray(ids)).to(
+            model.node_embedding.device), max_len)
+        if rows is not None:
+            return rows
     if isinstance(paths, np.ndarray) and paths.ndim == 2:
         rows = model.rows_of(paths.reshape(-1)).reshape(paths.shape)
         if not model.down_sampling and (rows >= 0).all():
