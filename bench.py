@@ -115,6 +115,10 @@ def secondary_rows(timeout_s=150):
                 if rf.get("traffic"):
                     row["traffic_GBps"] = rf["traffic"] / (rf["avg_kernel_ms"] / 1e3) / 1e9
             if wl == "c4":
+                row["community_kernel"] = j["config"]["community_kernel"]
+                row["roofline_peak"] = j["roofline"]["peak"]
+                row["roofline_peak_basis"] = j["roofline"].get("peak_basis")
+                row["frac_of_fp32_mfma_peak"] = j["roofline"].get("frac_of_fp32_mfma_peak")
                 for k in ("gmm_resp_kernel", "gmm_resp_ms", "gmm_resp_tflops_executed",
                           "gmm_scatter_ms",
                           "gmm_scatter_tflops_executed", "gmm_em_iteration_ms"):

@@ -5,7 +5,8 @@
                   (come_sgns_o1); metric pair-updates/s; roofline HBM, (3+n)*d*4 B per pair.
   --workload c4   BASELINE configs[3]: 1M nodes, K=50, d=128: the community-gradient pass
                   (come_community_grad, iters=1) and the GMM responsibility pass
-                  (come_gmm_resp); each 2*V*K*d^2 flops; roofline = fp32 MFMA peak 157.3 TFLOP/s.
+                  (come_gmm_resp); each 2*V*K*d^2 flops; roofline = fp32 MFMA peak 157.3 TFLOP/s
+                  (k_community_bf3: the bf16 MFMA peak / 6, its six bf16 part products per MAC).
   --workload walks  SURVEY.md §8f row 1, the producer of C3's input: one corpus pass over the C3
                   graph (1M-node power law, every node starts one walk, length 80) on the HIP
                   walker (come_random_walks); metric walk-steps/s; roofline: the measured 1.70
@@ -32,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA = f32 vector peak
+BF16_MFMA_PEAK_TFLOPS = 16 * F32_MFMA_PEAK_TFLOPS  # dense bf16 MFMA (~2.5 PF), 16x the f32 rate
 
 
 def log(*a):
@@ -179,8 +181,12 @@ def c4(args):
     tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
     cov_kernel = ("k_gmm_cov16" if opts.gmm_cov_async == 3 else "k_gmm_cov_async") if ct16 \
         else "VALU"
-    comm_kernel = ("k_community16" if opts.community_async == 2 else "k_community_async") \
-        if ct16 else "VALU"
+    comm_kernel = {1: "k_community_async", 2: "k_community16", 3: "k_community_bf3"}[
+        opts.community_async] if ct16 else "VALU"
+    # k_community_bf3 carries each fp32 operand as three bf16 parts and takes six part products
+    # per multiply-add: its ceiling is the bf16 MFMA peak / 6, not the fp32 MFMA peak
+    comm_bf3 = comm_kernel == "k_community_bf3"
+    comm_peak = BF16_MFMA_PEAK_TFLOPS / 6 if comm_bf3 else F32_MFMA_PEAK_TFLOPS
     resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp_mfma") if ct16 \
         else "VALU"
     x0 = x.clone()
@@ -276,8 +282,11 @@ def c4(args):
                    "gmm_scatter_tflops_executed": flops * tri_cov / ts / 1e12,
                    "gmm_em_iteration_ms": te * 1e3, **dist_cfg},
         "roofline": {"bound": "mfma", "achieved": flops / tg / 1e12 / world,
-                     "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (per GPU)",
-                     "frac": flops / tg / 1e12 / world / F32_MFMA_PEAK_TFLOPS,
+                     "peak": comm_peak, "unit": "TFLOP/s (per GPU)",
+                     "peak_basis": ("bf16 MFMA peak %.1f / 6 part products per fp32 multiply-add"
+                                    % BF16_MFMA_PEAK_TFLOPS) if comm_bf3 else "fp32 MFMA peak",
+                     "frac": flops / tg / 1e12 / world / comm_peak,
+                     "frac_of_fp32_mfma_peak": flops / tg / 1e12 / world / F32_MFMA_PEAK_TFLOPS,
                      "flops_per_pass": flops, "avg_kernel_ms": tg * 1e3},
         "cpu_baseline": cpu}))
 

@@ -34,7 +34,7 @@ extern "C" {
 #endif
 
 /* ABI 3 (this header): the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B
- * kernels) was removed, "community_async" accepts 1 / 2, "gmm_cov_async" 1 / 3 and "gmm_resp16"
+ * kernels) was removed, "community_async" accepts 1 / 2 / 3, "gmm_cov_async" 1 / 3 and "gmm_resp16"
  * 0 / 2 (other values: COME_E_INVALID at the call); come_source_sha256 was added.
  * ABI 2: come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
@@ -270,9 +270,12 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       d <= 128, n <= 5 -- compiled for 8 waves per SIMD there -- else 6)
  *   resident_cap        1 = also clamp grids to the workgroups the occupancy API reports resident
  *   community_async     community gradient at d = 64, 128 (16-B aligned mu / inv_cov; else the
- *                       VALU kernel): default 2 = k_community16 (16x16x4 MFMAs, one 16-row tile
- *                       per wavefront, 4 waves per SIMD; 11.57 vs 12.46 ms at C4); 1 = the 32x32x2
- *                       fallback k_community_async.  Other values: COME_E_INVALID
+ *                       VALU kernel): default 3 = k_community_bf3 (each fp32 operand as three
+ *                       bf16 parts, six exact part products per multiply-add on 32x32x16 bf16
+ *                       MFMAs -- fp32-level error, tests/test_gpu_c4.py; 7.3 vs 11.5 ms at C4);
+ *                       2 = k_community16 (fp32 16x16x4 MFMAs, one 16-row tile per wavefront);
+ *                       1 = the 32x32x2 fp32 fallback k_community_async.  Other values:
+ *                       COME_E_INVALID
  *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 3 = k_gmm_cov16 (16x16x4
  *                       tiles: 36 of 64 upper tiles at d = 128; 7.25 vs 7.92 ms at C4); 1 = the
  *                       32x32 fallback k_gmm_cov_async.  Other values: COME_E_INVALID

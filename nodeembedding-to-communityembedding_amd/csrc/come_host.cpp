@@ -142,7 +142,7 @@ static come_launch_opts g_opts = [] {
     // run's 0.97); at 100,000 nodes the cap is inactive (V/16 > occupancy) and NMI 0.99 either way.
     o.rows_per_wave = 16;
     o.o1_rows_per_wave = 12;
-    o.community_async = 2;
+    o.community_async = 3;
     o.gmm_cov_async = 3;
     o.gmm_resp16 = 2;
     o.o1_chunk = -1;

@@ -1,11 +1,12 @@
 #!/bin/bash
 # PMC passes over a short C4 run (bench_aux.py --workload c4): one rocprofv3 run per counter group.
+#   [C4_ARGS="--opt community_async=3"] [TAG=name] bash scripts/pmc_c4.sh "CTR1 CTR2" "CTR3" ...
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/pmc_c4"
+OUT="$ROOT/gpurun_out/pmc_c4${TAG:+_$TAG}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-RUN="$ROOT/bench_aux.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline"
+RUN="$ROOT/bench_aux.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ${C4_ARGS:-}"
 i=0
 for C in "$@"; do
   i=$((i+1))
@@ -20,8 +21,8 @@ disp = collections.defaultdict(set)
 for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         kn = r.get("Kernel_Name", "")
-        for tag in ("k_community_async", "k_community_mfma", "k_gmm_resp_mfma", "k_gmm_cov_async",
-                    "k_gmm_cov_mfma"):
+        for tag in ("k_community_async", "k_community16", "k_community_bf3", "k_gmm_resp16t",
+                    "k_gmm_resp_mfma", "k_gmm_cov_async", "k_gmm_cov16"):
             if tag in kn:
                 key = (tag, r["Counter_Name"])
                 agg[key] += float(r["Counter_Value"])

@@ -41,16 +41,23 @@ def c4_rows():
     return x, pi
 
 
-@pytest.mark.parametrize("iters", [1, 2])
-def test_c4_community_grad_k50_1m(c4_rows, iters):
+@pytest.mark.parametrize("iters,kern", [(1, 2), (2, 2), (1, 3), (2, 3)])
+def test_c4_community_grad_k50_1m(c4_rows, iters, kern):
     """x -= lr clip((beta/K) sum_k pi_ik inv_k (x_i - mu_k), +-5) (:61-78) on all 1M rows; 4,000
-    sampled rows (incl. the first and last row tile) against float64, `iters` rounds."""
+    sampled rows (incl. the first and last row tile) against float64, `iters` rounds;
+    community_async 2 (fp32 16x16x4 MFMAs) and 3 (fp32 operands as bf16 parts), one tolerance."""
+    from come_amd import _lib
     x0, pi = c4_rows
     w, mu, cov = params(4)
     inv = np.linalg.inv(cov.astype(np.float32)).astype(np.float32)  # :36, fp32 inverse
     beta, lr = 2.0 * K, 0.1  # beta/K = 2: some entries reach the +-5 clip
     x = t(x0)
-    ce.community_grad(x, t(pi), t(mu), t(inv), beta, lr, iters)
+    prev = _lib.launch_opts().community_async
+    _lib.set_option("community_async", kern)
+    try:
+        ce.community_grad(x, t(pi), t(mu), t(inv), beta, lr, iters)
+    finally:
+        _lib.set_option("community_async", prev)
     got = x.cpu().numpy()
     rng = np.random.RandomState(5)
     rows = np.concatenate([np.arange(64), rng.choice(len(x0), 3872, replace=False),
@@ -71,6 +78,42 @@ def test_c4_community_grad_k50_1m(c4_rows, iters):
     np.testing.assert_allclose(got[rows] - x0[rows], step, rtol=1e-4,
                                atol=1e-5 * np.abs(step).max())
     assert np.isfinite(got).all()
+
+
+def test_c4_community_bf3_error_is_fp32_level(c4_rows):
+    """k_community_bf3 carries each fp32 operand as three bf16 parts and sums six exact part
+    products per multiply-add (|dropped terms| < 2^-26 |a b|): a product more accurate than one
+    fp32 rounding, so its error against float64 must be that of the fp32-MFMA kernel
+    (k_community16), not a reduced-precision one.  Unclipped update (beta/K = 0.5, lr = 1) on
+    200k rows, all of them against float64: RMS and max error within 1.5x of k_community16's."""
+    from come_amd import _lib
+    x0, pi = c4_rows[0][:200_000], c4_rows[1][:200_000]
+    w, mu, cov = params(4)
+    inv = np.linalg.inv(cov.astype(np.float32)).astype(np.float32)
+    beta, lr = 0.5 * K, 1.0
+    X = x0.astype(np.float64)
+    G = np.zeros_like(X)
+    for k in range(K):
+        G += pi[:, k:k + 1].astype(np.float64) * ((X - mu[k].astype(np.float32)) @
+                                                  inv[k].astype(np.float64).T)
+    G *= beta / K
+    assert np.abs(G).max() < 5  # no clipping: the step is the gradient itself
+    step64 = -lr * G
+    errs = {}
+    prev = _lib.launch_opts().community_async
+    try:
+        for kern in (2, 3):
+            _lib.set_option("community_async", kern)
+            x = t(x0)
+            ce.community_grad(x, t(pi), t(mu), t(inv), beta, lr, 1)
+            e = (x.cpu().numpy().astype(np.float64) - X) - step64
+            errs[kern] = (np.sqrt((e ** 2).mean() / (step64 ** 2).mean()),
+                          np.abs(e).max() / np.abs(step64).max())
+    finally:
+        _lib.set_option("community_async", prev)
+    print("rms / max relative error vs float64: fp32 MFMA %.3g / %.3g, bf16 parts %.3g / %.3g"
+          % (errs[2] + errs[3]))
+    assert errs[3][0] <= 1.5 * errs[2][0] and errs[3][1] <= 1.5 * errs[2][1], errs
 
 
 def test_c4_responsibilities_k50_1m(c4_rows):

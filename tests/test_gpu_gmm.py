@@ -158,7 +158,7 @@ def test_variant_options_outside_the_kept_set_are_rejected():
         with opts(gmm_cov_async=bad):
             with pytest.raises(_lib.ComeError, match="gmm_cov_async"):
                 gmm.scatter(X, R, mp)
-    for bad in (0, 3):
+    for bad in (0, 4):
         with opts(community_async=bad):
             with pytest.raises(_lib.ComeError, match="community_async"):
                 ce.community_grad(X.clone(), R, mp, P, 0.01, 0.1, 1)
