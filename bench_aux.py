@@ -177,7 +177,8 @@ def c4(args):
     tri = (ct * (ct + 1) / 2) / (ct * ct) if ct else 1.0
     ct16 = d // 16 if d in (64, 128) else 0
     tri16 = (ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if ct16 else 1.0
-    tri_resp = (tri16 if opts.gmm_resp16 == 2 else tri) if ct16 else 1.0
+    tri_resp = (tri16 if opts.gmm_resp16 == 2 else
+                (ct * (ct + 1)) / (2 * ct * ct) if opts.gmm_resp16 == 3 else tri) if ct16 else 1.0
     tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
     cov_kernel = ("k_gmm_cov16" if opts.gmm_cov_async == 3 else "k_gmm_cov_async") if ct16 \
         else "VALU"
@@ -187,8 +188,8 @@ def c4(args):
     # per multiply-add: its ceiling is the bf16 MFMA peak / 6, not the fp32 MFMA peak
     comm_bf3 = comm_kernel == "k_community_bf3"
     comm_peak = BF16_MFMA_PEAK_TFLOPS / 6 if comm_bf3 else F32_MFMA_PEAK_TFLOPS
-    resp_kernel = ("k_gmm_resp16t" if opts.gmm_resp16 == 2 else "k_gmm_resp_mfma") if ct16 \
-        else "VALU"
+    resp_kernel = {0: "k_gmm_resp_mfma", 2: "k_gmm_resp16t", 3: "k_gmm_resp_bf3"}[
+        opts.gmm_resp16] if ct16 else "VALU"
     x0 = x.clone()
     xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]
 

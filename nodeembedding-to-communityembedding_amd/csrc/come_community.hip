@@ -1540,6 +1540,225 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
     }
 }
 
+// ---- E-step on bf16-part MFMAs (k_gmm_resp_bf3, gmm_resp16 = 3) -----------------------------
+//
+// k_community_bf3's arithmetic (fp32 operands as three bf16 parts, six exact part products per
+// multiply-add, summed in fp32) on Y = X P_k: output D[i][j] = Y[row j][32 ct + i] of column
+// tile ct, A = P_k^T parts (LDS), B = the row's x parts -- x does not change over the components,
+// so the row side is split ONCE per workgroup, not per component (k_community_bf3's VALU cost).
+// Upper factors only (sklearn's precisions_cholesky_): tile ct needs k-steps s <= 2 ct + 1, 20 of
+// the 32 (ct, s) blocks at d = 128 (6 of 8 at d = 64); a launch holding a lower or dense factor
+// returns at once and k_gmm_resp16_full runs it.  Each block's three parts are one 3 KiB image
+// (k_pack_upper_bf3); a component is staged in NU units of NB / NU blocks, two unit buffers, one
+// barrier per unit, mu_k P_k and log_norm_k beside it.  A row's sum of squares: 64 in-lane FMAs
+// and one permlane32 swap (the 32x32 accumulator holds 16 columns of one row per lane half).
+template <int D>
+struct RespBf3 {
+    static constexpr int NS = D / 16, CT = D / 32;
+    static constexpr int NB = CT * (CT + 1);  // sum over ct of 2 ct + 2
+    static constexpr int BLK = 3 * 1024;      // bytes per block image (3 parts x 32 rows x 32 B)
+    int ct[NB], s[NB];
+    constexpr RespBf3() : ct(), s() {
+        int n = 0;
+        for (int c = 0; c < CT; ++c)
+            for (int k = 0; k <= 2 * c + 1; ++k) {
+                ct[n] = c;
+                s[n] = k;
+                ++n;
+            }
+    }
+    // byte offset in a block image of (part P, row i, 16-B granule g), swizzled as CommBf3::at
+    __host__ __device__ static constexpr int at(int P, int i, int g) {
+        return P * 1024 + i * 32 + 16 * (g ^ ((i >> 4) & 1));
+    }
+};
+
+template <int D, int NW, int NU>
+struct RespBf3Shape {
+    static constexpr int NB = RespBf3<D>::NB;
+    // (NU even: unit t's buffer is t & 1 = u & 1, and component k + 1's parameters, staged with
+    // its first unit, never land in the buffer component k's epilogue is reading)
+    static_assert(NB % NU == 0 && NU % 2 == 0, "whole blocks per unit, an even unit count");
+    static constexpr int UB = NB / NU;                      // blocks per unit
+    static constexpr int UBYTES = UB * RespBf3<D>::BLK;
+    static constexpr int PAR = 2 * UBYTES;                  // par[2][256 + 64] floats: mu_k P_k, log_norm_k
+    static constexpr int PARF = 256 + 64;
+    static constexpr int LDS_BYTES = PAR + 2 * PARF * 4;
+    static constexpr int PIECES = UBYTES / 1024;
+};
+
+// the product shape: 4 wavefronts x 32 rows, four units of 5 blocks per component at d = 128
+// (4.65 / 4.68 ms vs 4.67 / 4.69 with two, profiles/r06_ab_estep_bf3.txt; A/B hooks below)
+#ifndef COME_RESP3_NW
+#define COME_RESP3_NW 4
+#endif
+#ifndef COME_RESP3_NU
+#define COME_RESP3_NU 4
+#endif
+template <int D>
+struct RespBf3Pick {
+    static constexpr int NW = COME_RESP3_NW;
+    static constexpr int NU = D == 64 ? 2 : COME_RESP3_NU;
+    using S = RespBf3Shape<D, NW, NU>;
+};
+
+// prec_chol [K][D][D] (upper) -> per component the NB block images of P_k^T's parts, block order
+// of RespBf3 (thread: one block row i and granule g = 8 consecutive features)
+template <int D>
+__global__ void __launch_bounds__(256) k_pack_upper_bf3(const float *__restrict__ P,
+                                                        char *__restrict__ img, int K) {
+    using R = RespBf3<D>;
+    constexpr R TB{};
+    const int64_t n = (int64_t)K * R::NB * 32 * 2;
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n;
+         t += (int64_t)gridDim.x * 256) {
+        const int g = (int)(t & 1), i = (int)((t >> 1) & 31);
+        const int64_t kb = t >> 6;  // k * NB + block
+        const int b = (int)(kb % R::NB);
+        const int64_t k = kb / R::NB;
+        const int c = 32 * TB.ct[b] + i, f0 = 16 * TB.s[b] + 8 * g;
+        const float *Pk = P + k * D * D;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = Pk[(int64_t)(f0 + e) * D + c];  // P^T[c][f] = P[f][c]
+        uint4 w[3];
+        uint32_t *w1 = &w[0].x, *w2 = &w[1].x, *w3 = &w[2].x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bf16_split3(v[2 * e], v[2 * e + 1], w1[e], w2[e], w3[e]);
+        char *blk = img + kb * R::BLK;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint4 *>(blk + R::at(p, i, g)) = w[p];
+    }
+}
+
+// unit t (component t / NU, unit t % NU) -> buffer b; with a component's first unit also its
+// mu_k P_k and log_norm_k -> par buffer k & 1
+template <int D, int NW, int NU>
+__device__ __forceinline__ void respbf3_stage(const RespArgs &a, const char *gimg, int64_t t,
+                                              char *smb, int b, int wid, int lane) {
+    using S = RespBf3Shape<D, NW, NU>;
+    const char *src = gimg + t * S::UBYTES + 16 * lane;
+#pragma unroll
+    for (int j = 0; j < (S::PIECES + NW - 1) / NW; ++j) {
+        const int i = wid + NW * j;
+        if (S::PIECES % NW != 0 && i >= S::PIECES) break;  // wavefront-uniform
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const float *>(src + i * 1024),
+                                         reinterpret_cast<float *>(smb + b * S::UBYTES + i * 1024),
+                                         16, 0, 0);
+    }
+    if (t % NU == 0) {
+        const int64_t k = t / NU;
+        float *par = reinterpret_cast<float *>(smb + S::PAR) + (k & 1) * S::PARF;
+        if (wid == 0) {
+            const int s = lane * 4 < D ? lane * 4 : D - 4;
+            __builtin_amdgcn_global_load_lds(a.mu_prec + k * D + s, par, 16, 0, 0);
+        } else if (wid == 1) {
+            __builtin_amdgcn_global_load_lds(a.log_norm + k, par + 256, 4, 0, 0);
+        }
+    }
+}
+
+template <int D, int NW, int NU>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
+    k_gmm_resp_bf3(RespArgs a) {
+    using R = RespBf3<D>;
+    using S = RespBf3Shape<D, NW, NU>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) char smb[];
+    if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0) return;
+    constexpr R TB{};
+    const char *gimg = reinterpret_cast<const char *>(a.prec_t);
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    const int64_t row = (int64_t)blockIdx.x * (32 * NW) + wid * 32 + j;
+    const bool rowok = row < a.V;
+    const int nt = a.K * NU;
+    respbf3_stage<D, NW, NU>(a, gimg, 0, smb, 0, wid, lane);
+    if (nt > 1) respbf3_stage<D, NW, NU>(a, gimg, 1, smb, 1, wid, lane);
+    // the row's parts, once: xp[s][P] = part P of features 16 s + 8 h .. + 7
+    bf16x8 xp[R::NS][3];
+#pragma unroll
+    for (int s = 0; s < R::NS; ++s) {
+        uint32_t w[3][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (rowok) v = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * s + 8 * h + 4 * u);
+            bf16_split3(v[0], v[1], w[0][2 * u], w[1][2 * u], w[2][2 * u]);
+            bf16_split3(v[2], v[3], w[0][2 * u + 1], w[1][2 * u + 1], w[2][2 * u + 1]);
+        }
+#pragma unroll
+        for (int P = 0; P < 3; ++P)
+            xp[s][P] = __builtin_bit_cast(bf16x8, uint4{w[P][0], w[P][1], w[P][2], w[P][3]});
+    }
+    const int aoff = R::at(0, j, h);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool owner = h == 0 && rowok;
+    float run_max = -INFINITY, run_sum = 0.0f, lp_prev = 0.0f;
+    for (int k = 0; k < a.K; ++k) {
+        // component k - 1's log-probability stored one component late (k_gmm_resp16t's reason)
+        if (k > 0 && owner) a.resp[row * a.K + k - 1] = lp_prev;
+        // sum over the row's columns of (Y - mu_k P_k)^2, tile by tile as each tile's last block
+        // completes (the VALU of tile ct beside the MFMAs of ct + 1): register r of tile ct is
+        // column 32 ct + (r & 3) + 8 (r >> 2) + 4 h
+        const float *par = reinterpret_cast<const float *>(smb + S::PAR) + (k & 1) * S::PARF;
+        float sq = 0.0f;
+        f32x16 acc[R::CT];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int t = k * NU + u;
+            const char *ub = smb + (u & 1) * S::UBYTES;  // t & 1
+#pragma unroll
+            for (int bi = 0; bi < S::UB; ++bi) {
+                const int b = u * S::UB + bi, ct = TB.ct[b], s = TB.s[b];
+                const char *base = ub + bi * R::BLK + aoff;
+                bf16x8 A[3];
+#pragma unroll
+                for (int P = 0; P < 3; ++P) A[P] = *reinterpret_cast<const bf16x8 *>(base + P * 1024);
+                // a tile's first block starts from the constant 0 (no accumulator reset)
+                const f32x16 c0 = s == 0 ? f32x16{} : acc[ct];
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], xp[s][0], c0, 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][2], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][0], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][0], acc[ct], 0, 0, 0);
+                if (s == 2 * ct + 1) {  // tile ct complete
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const f32x4 mp =
+                            *reinterpret_cast<const f32x4 *>(par + 32 * ct + 8 * g4 + 4 * h);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float y = acc[ct][4 * g4 + e] - mp[e];
+                            sq = __builtin_fmaf(y, y, sq);
+                        }
+                    }
+                }
+            }
+            if (t + 1 < nt) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();  // buffer t & 1 free; unit t + 1 (and its parameters) in LDS
+                if (t + 2 < nt) respbf3_stage<D, NW, NU>(a, gimg, t + 2, smb, u & 1, wid, lane);
+            }
+        }
+        const float lp = par[256] - 0.5f * reduce_stage<5>(sq);
+        lse_push(lp, run_max, run_sum);
+        lp_prev = lp;
+    }
+    if (owner) {
+        float *lp = a.resp + row * a.K;
+        lp[a.K - 1] = lp_prev;
+        const float lse = run_max + logf(run_sum);
+        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
+        if (a.lse) a.lse[row] = lse;
+    }
+}
+
 // The FULL body (k_gmm_resp16t's registers cannot hold it), launched after it: a no-op unless the
 // launch holds a lower or dense factor (flags[K]); row blocks grid-stride.
 template <int D>
@@ -2545,6 +2764,49 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         if (rc) return rc;
         a.prec_t = pt;
         const int r16 = current_opts().gmm_resp16;
+        if (r16 == 3) {
+            // default: k_gmm_resp_bf3 over the bf16-part images of the upper factors, then
+            // k_gmm_resp16_full (a no-op unless some factor is lower or dense)
+            using P64 = RespBf3Pick<64>;
+            using P128 = RespBf3Pick<128>;
+            const size_t img_bytes = (size_t)K * (d == 64 ? RespBf3<64>::NB : RespBf3<128>::NB) *
+                                     RespBf3<64>::BLK;
+            char *img = (char *)stream_scratch(dev, stream, kScratchRespSplit, img_bytes);
+            if (!img) return scratch_failed();
+            const int64_t work = (int64_t)K * (d == 64 ? RespBf3<64>::NB : RespBf3<128>::NB) * 64;
+            hipLaunchKernelGGL(d == 64 ? k_pack_upper_bf3<64> : k_pack_upper_bf3<128>,
+                               dim3((unsigned)std::min<int64_t>((work + 255) / 256, 4096)),
+                               dim3(256), 0, (hipStream_t)stream, prec_chol, img, K);
+            rc = hip_error(hipGetLastError(), "k_pack_upper_bf3 launch");
+            if (rc) return rc;
+            RespArgs b = a;
+            b.prec_full = a.prec_t;
+            b.prec_t = reinterpret_cast<const float *>(img);
+            void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_bf3<64, P64::NW, P64::NU>
+                                             : k_gmm_resp_bf3<128, P128::NW, P128::NU>;
+            static bool attr3 = false;
+            if (!attr3) {
+                for (void (*f)(RespArgs) : {k_gmm_resp_bf3<64, P64::NW, P64::NU>,
+                                            k_gmm_resp_bf3<128, P128::NW, P128::NU>,
+                                            k_gmm_resp16_full<64>, k_gmm_resp16_full<128>})
+                    (void)hipFuncSetAttribute((const void *)f,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr3 = true;
+            }
+            const int nw = d == 64 ? P64::NW : P128::NW;
+            hipLaunchKernelGGL(kern, dim3((unsigned)((V + 32 * nw - 1) / (32 * nw))), dim3(64 * nw),
+                               d == 64 ? P64::S::LDS_BYTES : P128::S::LDS_BYTES, (hipStream_t)stream,
+                               b);
+            rc = hip_error(hipGetLastError(), "k_gmm_resp_bf3 launch");
+            if (rc) return rc;
+            const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
+                                                                   : Resp16Shape<128>::LDS);
+            const int64_t blks = (V + 127) / 128;
+            hipLaunchKernelGGL(d == 64 ? k_gmm_resp16_full<64> : k_gmm_resp16_full<128>,
+                               dim3((unsigned)std::min<int64_t>(blks, 2 * (int64_t)num_cus(dev))),
+                               dim3(256), lds16, (hipStream_t)stream, b);
+            return hip_error(hipGetLastError(), "k_gmm_resp16_full launch");
+        }
         if (r16 == 2) {
             // default: k_gmm_resp16t over the packed non-zero blocks (every factor upper-
             // triangular), then k_gmm_resp16_full (a no-op unless some factor is lower or dense)
@@ -2583,7 +2845,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
             return hip_error(hipGetLastError(), "k_gmm_resp16_full launch");
         }
         if (r16 != 0)
-            return set_error(COME_E_INVALID, "gmm_resp16 must be 0 or 2 (got %d)", r16);
+            return set_error(COME_E_INVALID, "gmm_resp16 must be 0, 2 or 3 (got %d)", r16);
         // 0: the 32x32x2 fallback k_gmm_resp_mfma
         const unsigned grid = (unsigned)((V + 127) / 128);
         const size_t lds = sizeof(float) * (size_t)(d == 64 ? RespShape<64>::LDS

@@ -29,7 +29,8 @@ int64_t *launch_counter(int device, void *stream);
 // a stream only after a warm-up call of the same shape -- a growth during capture is refused).
 // nullptr on failure, with the error message set: return scratch_failed() (its status code).
 constexpr int kScratchGmmFlags = 0, kScratchGmmPt = 1, kScratchHotCounts = 2, kScratchHotBits = 3,
-              kScratchGmmTri = 4, kScratchCommSplit = 5, kScratchSlots = 6;
+              kScratchGmmTri = 4, kScratchCommSplit = 5, kScratchRespSplit = 6,
+              kScratchSlots = 7;
 float *stream_scratch(int device, void *stream, int slot, size_t bytes);
 int scratch_failed();
 // The contended-row bitmap a Hogwild launch uses when the caller passes none (come_hot.hip):

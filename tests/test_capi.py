@@ -77,7 +77,7 @@ def test_launch_options_snapshot_and_per_call_struct():
     L = _lib.lib()
     o = _lib.launch_opts()
     assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 3
-    assert o.gmm_resp16 == 2
+    assert o.gmm_resp16 == 3
     assert o.o1_chunk == -1 and o.community_async == 3
     assert o.o2_update_count is None
     _lib.set_option("max_waves", 77)

@@ -116,10 +116,55 @@ def test_c4_community_bf3_error_is_fp32_level(c4_rows):
     assert errs[3][0] <= 1.5 * errs[2][0] and errs[3][1] <= 1.5 * errs[2][1], errs
 
 
-def test_c4_responsibilities_k50_1m(c4_rows):
+@pytest.mark.parametrize("r16", [2, 3])
+def test_c4_responsibilities_k50_1m(c4_rows, r16):
     """predict_proba (:37) of a K = 50 full-covariance mixture on all 1M rows (come_gmm_resp,
     sklearn's upper-triangular precision factors) and the EM E-step (come_gmm_estep, + per-row
-    log-sum-exp) on 4,000 sampled rows against the float64 restatement of sklearn."""
+    log-sum-exp) on 4,000 sampled rows against the float64 restatement of sklearn;
+    gmm_resp16 2 (fp32 16x16x4 MFMAs) and 3 (fp32 operands as bf16 parts), one tolerance."""
+    from come_amd import _lib
+    prev = _lib.launch_opts().gmm_resp16
+    _lib.set_option("gmm_resp16", r16)
+    try:
+        _c4_responsibilities(c4_rows)
+    finally:
+        _lib.set_option("gmm_resp16", prev)
+
+
+def test_c4_estep_bf3_error_is_fp32_level(c4_rows):
+    """k_gmm_resp_bf3's per-row log-sum-exp (the EM log-likelihood term) against float64 on 100k
+    C4 rows: RMS and max error within 1.5x of the fp32-MFMA E-step's (k_gmm_resp16t) -- the
+    bf16-part products are not a reduced-precision form (see the community test above)."""
+    from come_amd import _lib
+    from scipy.special import logsumexp
+    x0 = c4_rows[0][:100_000]
+    w, mu, cov = params(6, sep=0.3)
+    pc = orc.precision_cholesky(cov)
+    g = gmm.GaussianMixture(K)
+    g._w, g._mu, g._pc = (torch.as_tensor(a, device=DEV) for a in (w, mu, pc))
+    g._prepare_estep()
+    pcf = g._e_pc.double().cpu().numpy()
+    mpf = g._e_mp.double().cpu().numpy()
+    lnf = g._e_ln.double().cpu().numpy()
+    X = x0.astype(np.float64)
+    lp = np.stack([lnf[k] - 0.5 * ((X @ pcf[k] - mpf[k]) ** 2).sum(1) for k in range(K)], 1)
+    ref = logsumexp(lp, 1)
+    errs = {}
+    prev = _lib.launch_opts().gmm_resp16
+    try:
+        for r16 in (2, 3):
+            _lib.set_option("gmm_resp16", r16)
+            _, lse = gmm.estep(t(x0), g._e_pc, g._e_mp, g._e_ln)
+            e = lse.double().cpu().numpy() - ref
+            errs[r16] = (np.sqrt((e ** 2).mean() / (ref ** 2).mean()), np.abs(e).max())
+    finally:
+        _lib.set_option("gmm_resp16", prev)
+    print("lse rms relative / max abs error vs float64: fp32 MFMA %.3g / %.3g, bf16 parts "
+          "%.3g / %.3g" % (errs[2] + errs[3]))
+    assert errs[3][0] <= 1.5 * errs[2][0] and errs[3][1] <= 1.5 * errs[2][1], errs
+
+
+def _c4_responsibilities(c4_rows):
     x0, _ = c4_rows
     w, mu, cov = params(6, sep=0.3)
     pc = orc.precision_cholesky(cov)

@@ -81,14 +81,14 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("r16", [0, 2])
+@pytest.mark.parametrize("r16", [0, 2, 3])
 def test_estep_mixed_factor_shapes(d, r16):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
     loop.  Mixed in one launch, every component must match the float64 quadratic form -- for the
-    default k_gmm_resp16t (gmm_resp16 = 2: a lower or dense factor in the launch sends every
-    component to the separate k_gmm_resp16_full launch) and the 32x32 fallback k_gmm_resp_mfma
-    (gmm_resp16 = 0: per-component flags)."""
+    bf16-part k_gmm_resp_bf3 (gmm_resp16 = 3) and k_gmm_resp16t (= 2) -- a lower or dense factor
+    in the launch sends every component to the separate k_gmm_resp16_full launch -- and the 32x32
+    fallback k_gmm_resp_mfma (gmm_resp16 = 0: per-component flags)."""
     V, K = 1500, 6
     rng = np.random.RandomState(d)
     X = rng.standard_normal((V, d)).astype(np.float32)
@@ -116,9 +116,10 @@ def test_estep_mixed_factor_shapes(d, r16):
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (70_001, 7, 64), (300, 3, 64), (129, 1, 128),
                                    (1, 4, 128), (5000, 2, 128)])
 def test_estep_default_and_fallback_agree(V, K, d):
-    """The default E-step (k_gmm_resp16t, 16-wide blocks) and the 32x32 fallback
-    (k_gmm_resp_mfma) on sklearn-shaped upper factors, ragged row counts: the same quantities
-    summed in different orders -- equal to float tolerance, responsibilities summing to 1."""
+    """The E-step forms -- k_gmm_resp_bf3 (bf16 parts), k_gmm_resp16t (16-wide fp32 blocks) and
+    the 32x32 fallback k_gmm_resp_mfma -- on sklearn-shaped upper factors, ragged row counts: the
+    same quantities summed in different orders, equal to float tolerance, responsibilities summing
+    to 1."""
     rng = np.random.RandomState(V + 7 * K)
     X = rng.standard_normal((V, d)).astype(np.float32)
     P = np.stack([np.triu(rng.standard_normal((d, d)) / np.sqrt(d)) + 2 * np.eye(d)
@@ -128,13 +129,14 @@ def test_estep_default_and_fallback_agree(V, K, d):
     ln = np.log(rng.dirichlet(np.ones(K)))
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
     out = {}
-    for r16 in (2, 0):
+    for r16 in (3, 2, 0):
         with opts(gmm_resp16=r16):
             resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
         out[r16] = resp.cpu().numpy(), lse.cpu().numpy()
-    assert np.isfinite(out[2][0]).all() and np.abs(out[2][0].sum(1) - 1).max() < 1e-4
-    np.testing.assert_allclose(out[2][0], out[0][0], atol=1e-4)
-    np.testing.assert_allclose(out[2][1], out[0][1], rtol=1e-5, atol=1e-3)
+    for r16 in (3, 2):
+        assert np.isfinite(out[r16][0]).all() and np.abs(out[r16][0].sum(1) - 1).max() < 1e-4
+        np.testing.assert_allclose(out[r16][0], out[0][0], atol=1e-4)
+        np.testing.assert_allclose(out[r16][1], out[0][1], rtol=1e-5, atol=1e-3)
 
 
 def test_variant_options_outside_the_kept_set_are_rejected():
@@ -150,7 +152,7 @@ def test_variant_options_outside_the_kept_set_are_rejected():
     P = t(np.stack([np.eye(d)] * K))
     mp, ln = t(np.zeros((K, d))), t(np.log(np.full(K, 1.0 / K)))
     R = t(rng.dirichlet(np.ones(K), V))
-    for bad in (1, 3, 7, 16, 19):
+    for bad in (1, 4, 7, 16, 19):
         with opts(gmm_resp16=bad):
             with pytest.raises(_lib.ComeError, match="gmm_resp16"):
                 gmm.estep(X, P, mp, ln)
@@ -314,9 +316,9 @@ def test_community2vec_trains_at_d256():
 
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (1000, 5, 128), (2049, 9, 64), (300, 3, 64),
                                    (129, 1, 128)])
-@pytest.mark.parametrize("r16", [0, 2])
+@pytest.mark.parametrize("r16", [0, 2, 3])
 def test_estep_upper_factors_vs_float64(V, K, d, r16):
-    """The default k_gmm_resp16t (gmm_resp16 = 2) and the fallback k_gmm_resp_mfma (= 0) with
+    """k_gmm_resp_bf3 (gmm_resp16 = 3), k_gmm_resp16t (= 2) and the fallback k_gmm_resp_mfma (= 0) with
     sklearn-shaped (upper-triangular) precision factors only -- the launches that take the
     triangular skip -- against the float64 quadratic form, ragged rows."""
     from scipy.special import logsumexp
