@@ -180,8 +180,8 @@ def c4(args):
     tri_resp = (tri16 if opts.gmm_resp16 == 2 else
                 (ct * (ct + 1)) / (2 * ct * ct) if opts.gmm_resp16 == 3 else tri) if ct16 else 1.0
     tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
-    cov_kernel = ("k_gmm_cov16" if opts.gmm_cov_async == 3 else "k_gmm_cov_async") if ct16 \
-        else "VALU"
+    cov_kernel = {1: "k_gmm_cov_async", 3: "k_gmm_cov16", 4: "k_gmm_cov_bf3"}[
+        opts.gmm_cov_async] if ct16 else "VALU"
     comm_kernel = {1: "k_community_async", 2: "k_community16", 3: "k_community_bf3"}[
         opts.community_async] if ct16 else "VALU"
     # k_community_bf3 carries each fp32 operand as three bf16 parts and takes six part products

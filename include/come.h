@@ -34,7 +34,7 @@ extern "C" {
 #endif
 
 /* ABI 3 (this header): the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B
- * kernels) was removed, "community_async" accepts 1 / 2 / 3, "gmm_cov_async" 1 / 3 and "gmm_resp16"
+ * kernels) was removed, "community_async" accepts 1 / 2 / 3, "gmm_cov_async" 1 / 3 / 4 and "gmm_resp16"
  * 0 / 2 / 3 (other values: COME_E_INVALID at the call); come_source_sha256 was added.
  * ABI 2: come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
@@ -276,9 +276,12 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       2 = k_community16 (fp32 16x16x4 MFMAs, one 16-row tile per wavefront);
  *                       1 = the 32x32x2 fp32 fallback k_community_async.  Other values:
  *                       COME_E_INVALID
- *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 3 = k_gmm_cov16 (16x16x4
- *                       tiles: 36 of 64 upper tiles at d = 128; 7.25 vs 7.92 ms at C4); 1 = the
- *                       32x32 fallback k_gmm_cov_async.  Other values: COME_E_INVALID
+ *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 4 = k_gmm_cov_bf3 (E^T E with
+ *                       E = sqrt(r) (x - m) carried as three bf16 parts, six exact part products
+ *                       per multiply-add on 32x32x16 bf16 MFMAs, 10 upper 32x32 tiles; 5.62 ms at
+ *                       C4); 3 = k_gmm_cov16 (fp32 16x16x4 tiles: 36 of 64 upper tiles at d =
+ *                       128; 7.22 ms); 1 = the 32x32 fp32 fallback k_gmm_cov_async (7.92 ms).
+ *                       Other values: COME_E_INVALID
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)

@@ -2419,6 +2419,215 @@ __global__ void __launch_bounds__((Cov16<D>::THREADS))
     }
 }
 
+// ---- M-step scatter on bf16-part MFMAs (k_gmm_cov_bf3, gmm_cov_async = 4) --------------------
+//
+// S_k = sum_i r_ik d_i d_i^T (d_i = x_i - m_k) written as E^T E with E_ik = sqrt(r_ik) d_i: one
+// operand image serves both sides of every MFMA.  E is formed and split into its three bf16 parts
+// (k_community_bf3's arithmetic: six exact part products per multiply-add, summed in fp32) by 4
+// staging wavefronts, ONCE per (sample, feature, component), into a feature-major LDS image (rows
+// of 32 samples, 16-byte granules of 8 samples XOR-swizzled by CovBf3::swz: conflict-free
+// ds_read_b128 fragments and ds_write_b128 stores).  The MFMA wavefronts take fragment a (32
+// features x 16 samples, one ds_read_b128 per part) as the A operand of the tiles in row a and
+// the B operand of the tiles in column a: the 10 upper 32x32 tiles of a d = 128 component (3 at
+// d = 64) split 5 / 5 over two wavefronts.  sqrt(r) adds one rounding (1 ulp) to each weight
+// against the fp32 kernels' r d: tests hold the result to their tolerances and error level.
+// Grid and output as k_gmm_cov16 (components per workgroup x row chunks, [chunk][K][d][d]).
+template <int D>
+struct CovBf3 {
+    static constexpr int RB = 32;                   // samples per block (2 k-steps)
+    static constexpr int CPW = D == 128 ? 2 : 4;    // components per workgroup
+    static constexpr int WPC = D == 128 ? 2 : 1;    // MFMA wavefronts per component
+    static constexpr int AW = CPW * WPC;            // MFMA wavefronts (4)
+    static constexpr int THREADS = 64 * (AW + 4);   // + 4 staging wavefronts
+    static constexpr int NTW = D == 128 ? 5 : 3;    // tiles per MFMA wavefront
+    static constexpr int NF = D / 32;               // fragments (32-feature row groups)
+    static constexpr int PLANE = D * RB * 2;        // bytes per part image (D rows x 32 bf16)
+    static constexpr int IMG = 3 * PLANE;           // per component (24 KB at d = 128)
+    static constexpr int BUF = CPW * IMG;
+    static constexpr int LDS_BYTES = 2 * BUF;       // 96 KB: one workgroup per CU
+    static constexpr int SPT = RB * D / 256;        // samples per staging thread (16 / 8)
+    // granule swizzle: bit 0 = bit 2 of the row, bit 1 = bit 1 ^ bit 3 -- distinct over the rows
+    // of every 16-lane ds_read_b128 group (64 banks) and of every 8-lane ds_write_b128 group (32
+    // banks: 8 consecutive rows) that share a bank column
+    __host__ __device__ static constexpr int swz(int f) {
+        return ((f >> 2) & 1) | ((((f >> 1) ^ (f >> 3)) & 1) << 1);
+    }
+    __host__ __device__ static constexpr int at(int P, int f, int g) {
+        return P * PLANE + f * 64 + 16 * (g ^ swz(f));
+    }
+};
+
+// tile n of MFMA part p: (row group ta, column group tb), ta <= tb
+template <int D>
+struct CovBf3Tiles {
+    int ta[2][5], tb[2][5];
+    constexpr CovBf3Tiles() : ta(), tb() {
+        if (D == 128) {
+            const int a0[5] = {0, 0, 0, 0, 3}, b0[5] = {0, 1, 2, 3, 3};
+            const int a1[5] = {1, 1, 1, 2, 2}, b1[5] = {1, 2, 3, 2, 3};
+            for (int n = 0; n < 5; ++n) {
+                ta[0][n] = a0[n];
+                tb[0][n] = b0[n];
+                ta[1][n] = a1[n];
+                tb[1][n] = b1[n];
+            }
+        } else {
+            const int a0[3] = {0, 0, 1}, b0[3] = {0, 1, 1};
+            for (int n = 0; n < 3; ++n) {
+                ta[0][n] = a0[n];
+                tb[0][n] = b0[n];
+            }
+        }
+    }
+};
+
+template <int D, int P>
+__device__ __forceinline__ void covbf3_part(const CovArgs &a, const char *smb, int nb, int tk,
+                                            int nk, int k0, int64_t chunk, int lane) {
+    using C = CovBf3<D>;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr CovBf3Tiles<D> TT{};
+    const int i = lane & 31, h = lane >> 5;
+    f32x16 acc[C::NTW];
+#pragma unroll
+    for (int n = 0; n < C::NTW; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[n][e] = 0.0f;
+    // which fragments this part reads (part 1 of d = 128 never needs fragment 0)
+    constexpr bool need0 = !(D == 128 && P == 1);
+    for (int j = 0; j < nb; ++j) {
+        __syncthreads();  // barrier j: block j staged
+        const char *im = smb + (j & 1) * C::BUF + tk * C::IMG;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            bf16x8 F[C::NF][3];
+#pragma unroll
+            for (int f = 0; f < C::NF; ++f) {
+                if (f == 0 && !need0) continue;
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    F[f][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * f + i, 2 * st + h));
+            }
+#pragma unroll
+            for (int n = 0; n < C::NTW; ++n) {
+                const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][2], F[tb][0], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][0], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
+            }
+        }
+    }
+    if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+    float *out = a.out + (chunk * a.K + k0 + tk) * D * D;
+#pragma unroll
+    for (int n = 0; n < C::NTW; ++n) {
+        const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+        const int jj = 32 * tb + i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int ii = 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+            out[(int64_t)ii * D + jj] = acc[n][r];
+            if (ta != tb) out[(int64_t)jj * D + ii] = acc[n][r];
+        }
+    }
+}
+
+// staging thread st: feature f = st % D of samples SPT sg .. SPT sg + SPT - 1 (sg = st / D,
+// uniform over a wavefront); lane l < CPW SPT of each wavefront also loads the weight r of its
+// (component l / SPT, sample l % SPT), square-rooted at stage time and broadcast by readlane
+// (a broadcast through a 128-byte LDS slot per wavefront instead -- one store, 8 ds_read_b128 --
+// was 3% slower: 5.80-5.88 vs 5.64-5.71 ms at C4)
+template <int D>
+struct CovBf3Stage {
+    using C = CovBf3<D>;
+    static constexpr int SPT = C::SPT, CPW = C::CPW;
+    static constexpr int NS = 3;  // register sets: loads run NS blocks ahead
+    const CovArgs &a;
+    const int f, sg, k0, nk, lane;
+    const int64_t c0, c1;
+    float mu[CPW];
+    float xv[NS][SPT];
+    float wv[NS];
+    __device__ __forceinline__ CovBf3Stage(const CovArgs &a_, int st, int lane_, int k0_, int nk_,
+                                           int64_t c0_, int64_t c1_)
+        : a(a_), f(st % D), sg(__builtin_amdgcn_readfirstlane(st / D)), k0(k0_), nk(nk_),
+          lane(lane_), c0(c0_), c1(c1_) {
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+            mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + f] : 0.0f;
+    }
+    // unconditional loads (rows clamped to the chunk, components to K - 1; zeroed when staged)
+    __device__ __forceinline__ void load(int u, int blk) {
+        const int64_t b = c0 + (int64_t)blk * C::RB + SPT * sg;
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) xv[u][q] = a.x[min(b + q, c1 - 1) * D + f];
+        const int l = lane % (CPW * SPT);
+        wv[u] = a.resp[min(b + l % SPT, c1 - 1) * a.K + min(k0 + l / SPT, a.K - 1)];
+    }
+    // the weight of lane l's (component, sample): sqrt(r), 0 past the chunk or K (so every E
+    // value of those is an exact 0 with no per-element select; x is finite, rows clamped)
+    __device__ __forceinline__ float weight(int u, int blk) const {
+        const int l = lane % (CPW * SPT);
+        const int64_t row = c0 + (int64_t)blk * C::RB + SPT * sg + l % SPT;
+        return (l / SPT < nk && row < c1) ? sqrtf(wv[u]) : 0.0f;
+    }
+    __device__ __forceinline__ void stage(float *img, int u, int blk) const {
+        char *buf = reinterpret_cast<char *>(img) + (blk % 2) * C::BUF;
+        const float w = weight(u, blk);
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk) {
+            char *im = buf + kk * C::IMG;
+#pragma unroll
+            for (int g = 0; g < SPT / 8; ++g) {
+                uint32_t p1[4], p2[4], p3[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v[2];
+#pragma unroll
+                    for (int z = 0; z < 2; ++z) {
+                        const int q = 8 * g + 2 * e + z;
+                        const float ws =
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), kk * SPT + q));
+                        v[z] = ws * (xv[u][q] - mu[kk]);
+                    }
+                    bf16_split3(v[0], v[1], p1[e], p2[e], p3[e]);
+                }
+                const int gr = (SPT * sg) / 8 + g;  // granule of the 32-sample row
+                *reinterpret_cast<uint4 *>(im + C::at(0, f, gr)) = uint4{p1[0], p1[1], p1[2], p1[3]};
+                *reinterpret_cast<uint4 *>(im + C::at(1, f, gr)) = uint4{p2[0], p2[1], p2[2], p2[3]};
+                *reinterpret_cast<uint4 *>(im + C::at(2, f, gr)) = uint4{p3[0], p3[1], p3[2], p3[3]};
+            }
+        }
+    }
+};
+
+template <int D>
+__global__ void __launch_bounds__(CovBf3<D>::THREADS) __attribute__((amdgpu_waves_per_eu(2)))
+    k_gmm_cov_bf3(CovArgs a) {
+    using C = CovBf3<D>;
+    extern __shared__ __attribute__((aligned(16))) char smb[];
+    const int64_t chunk = blockIdx.y;
+    const int k0 = blockIdx.x * C::CPW;
+    const int nk = a.K - k0 < C::CPW ? a.K - k0 : C::CPW;
+    const int64_t c0 = chunk * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int nb = c1 > c0 ? (int)((c1 - c0 + C::RB - 1) / C::RB) : 0;
+    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wid < C::AW) {
+        const int tk = wid / C::WPC, p = wid % C::WPC;
+        if (p == 0) covbf3_part<D, 0>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else covbf3_part<D, (C::WPC > 1 ? 1 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        return;
+    }
+    CovBf3Stage<D> sg(a, tid - 64 * C::AW, lane, k0, nk, c0, c1);
+    cov16_staging<D>(reinterpret_cast<float *>(smb), sg, nb);
+}
+
 // Any d <= 128 on the VALU: thread owns entries tid + 256 q of the d x d output.
 __global__ void __launch_bounds__(256) k_gmm_cov_valu(CovArgs a) {
     constexpr int MAXQ = 64;  // 128 * 128 / 256
@@ -2922,10 +3131,31 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
-    // gmm_cov_async: 3 (default) = k_gmm_cov16, 1 = the 32x32 fallback k_gmm_cov_async
+    // gmm_cov_async: 4 (default) = k_gmm_cov_bf3 (bf16 parts), 3 = k_gmm_cov16 (fp32 16x16x4),
+    // 1 = the 32x32 fp32 fallback k_gmm_cov_async
     const int cv = current_opts().gmm_cov_async;
-    if (cv != 1 && cv != 3)
-        return set_error(COME_E_INVALID, "gmm_cov_async must be 1 or 3 (got %d)", cv);
+    if (cv != 1 && cv != 3 && cv != 4)
+        return set_error(COME_E_INVALID, "gmm_cov_async must be 1, 3 or 4 (got %d)", cv);
+    if (mfma && cv == 4) {
+        static bool attr4 = false;
+        if (!attr4) {
+            for (void (*f)(CovArgs) : {k_gmm_cov_bf3<64>, k_gmm_cov_bf3<128>})
+                (void)hipFuncSetAttribute((const void *)f,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr4 = true;
+        }
+        const int cpw = d == 64 ? CovBf3<64>::CPW : CovBf3<128>::CPW;
+        hipLaunchKernelGGL(d == 64 ? k_gmm_cov_bf3<64> : k_gmm_cov_bf3<128>,
+                           dim3((K + cpw - 1) / cpw, used),
+                           dim3(d == 64 ? CovBf3<64>::THREADS : CovBf3<128>::THREADS),
+                           d == 64 ? CovBf3<64>::LDS_BYTES : CovBf3<128>::LDS_BYTES,
+                           (hipStream_t)stream, a);
+        rc = hip_error(hipGetLastError(), "k_gmm_cov_bf3 launch");
+        if (rc || used == 1) return rc;
+        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+    }
     void (*kern)(CovArgs) = !mfma     ? k_gmm_cov_valu
                             : cv == 3 ? (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>)
                                       : (d == 64 ? k_gmm_cov_async<64> : k_gmm_cov_async<128>);

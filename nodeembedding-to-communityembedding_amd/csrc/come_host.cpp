@@ -143,7 +143,7 @@ static come_launch_opts g_opts = [] {
     o.rows_per_wave = 16;
     o.o1_rows_per_wave = 12;
     o.community_async = 3;
-    o.gmm_cov_async = 3;
+    o.gmm_cov_async = 4;
     o.gmm_resp16 = 3;
     o.o1_chunk = -1;
     o.walk_staged = 1;

@@ -76,7 +76,7 @@ def test_launch_options_snapshot_and_per_call_struct():
     ctypes LaunchOpts mirrors come_launch_opts field for field; unknown names are rejected."""
     L = _lib.lib()
     o = _lib.launch_opts()
-    assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 3
+    assert o.rows_per_wave == 16 and o.o1_rows_per_wave == 12 and o.gmm_cov_async == 4
     assert o.gmm_resp16 == 3
     assert o.o1_chunk == -1 and o.community_async == 3
     assert o.o2_update_count is None

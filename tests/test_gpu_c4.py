@@ -200,20 +200,53 @@ def c4_100k():
     return X.astype(np.float32), w, mu, cov
 
 
-def test_c4_scatter_k50(c4_100k):
+@pytest.mark.parametrize("cov", [3, 4])
+def test_c4_scatter_k50(c4_100k, cov):
     """M-step scatter matrices sum_i r_ik (x_i - m_k)(x_i - m_k)^T (come_gmm_scatter, the
     2-component async MFMA workgroups, K = 50 = 25 pairs) vs float64 for a spread of
-    components, both members of a workgroup pair included."""
-    X, w, mu, cov = c4_100k
+    components, both members of a workgroup pair included; gmm_cov_async 3 (fp32 16x16x4) and 4
+    (bf16 parts)."""
+    from come_amd import _lib
+    X, w, mu, cov_ = c4_100k
     R = np.random.RandomState(10).dirichlet(np.ones(K), len(X)).astype(np.float32)
     M = (mu + 0.1).astype(np.float32)
-    S = gmm.scatter(t(X), t(R), t(M)).cpu().numpy()
+    prev = _lib.launch_opts().gmm_cov_async
+    _lib.set_option("gmm_cov_async", cov)
+    try:
+        S = gmm.scatter(t(X), t(R), t(M)).cpu().numpy()
+    finally:
+        _lib.set_option("gmm_cov_async", prev)
     X64 = X.astype(np.float64)
     for k in (0, 1, 24, 25, 48, 49):
         Dk = X64 - M[k]
         ref = (R[:, k, None] * Dk).T @ Dk
         np.testing.assert_allclose(S[k], ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max(),
                                    err_msg="component %d" % k)
+
+
+def test_c4_scatter_bf3_error_is_fp32_level(c4_100k):
+    """k_gmm_cov_bf3 (E^T E with E = sqrt(r) (x - m) carried as three bf16 parts) against
+    float64 on the 100k C4 rows, all 50 components: RMS and max relative error within 1.5x of
+    the fp32-MFMA scatter's (k_gmm_cov16)."""
+    from come_amd import _lib
+    X, w, mu, cov_ = c4_100k
+    R = np.random.RandomState(10).dirichlet(np.ones(K), len(X)).astype(np.float32)
+    M = (mu + 0.1).astype(np.float32)
+    X64 = X.astype(np.float64)
+    ref = np.stack([((R[:, k, None] * (X64 - M[k])).T @ (X64 - M[k])) for k in range(K)])
+    errs = {}
+    prev = _lib.launch_opts().gmm_cov_async
+    try:
+        for cv in (3, 4):
+            _lib.set_option("gmm_cov_async", cv)
+            e = gmm.scatter(t(X), t(R), t(M)).double().cpu().numpy() - ref
+            errs[cv] = (np.sqrt((e ** 2).mean() / (ref ** 2).mean()),
+                        np.abs(e).max() / np.abs(ref).max())
+    finally:
+        _lib.set_option("gmm_cov_async", prev)
+    print("scatter rms / max relative error vs float64: fp32 MFMA %.3g / %.3g, bf16 parts "
+          "%.3g / %.3g" % (errs[3] + errs[4]))
+    assert errs[4][0] <= 1.5 * errs[3][0] and errs[4][1] <= 1.5 * errs[3][1], errs
 
 
 def test_c4_em_iterations_k50_match_sklearn(c4_100k):

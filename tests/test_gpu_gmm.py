@@ -156,7 +156,7 @@ def test_variant_options_outside_the_kept_set_are_rejected():
         with opts(gmm_resp16=bad):
             with pytest.raises(_lib.ComeError, match="gmm_resp16"):
                 gmm.estep(X, P, mp, ln)
-    for bad in (0, 2, 4):
+    for bad in (0, 2, 5):
         with opts(gmm_cov_async=bad):
             with pytest.raises(_lib.ComeError, match="gmm_cov_async"):
                 gmm.scatter(X, R, mp)
@@ -169,7 +169,7 @@ def test_variant_options_outside_the_kept_set_are_rejected():
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
                                           (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None),
                                           (1500, 3, 256, 4), (200, 2, 330, None)])
-@pytest.mark.parametrize("cov", [1, 3])
+@pytest.mark.parametrize("cov", [1, 3, 4])
 def test_scatter_vs_numpy(V, K, d, chunks, cov):
     rng = np.random.RandomState(V + K)
     X = rng.normal(size=(V, d)).astype(np.float32)
@@ -268,7 +268,8 @@ def test_community2vec_distributed_flag_single_process_matches():
                                           (5000, 3, 64, None), (65, 4, 64, 2), (700, 1, 128, 3),
                                           (517, 7, 64, 2), (1031, 9, 64, None)])
 def test_scatter_default_and_fallback_agree(V, K, d, chunks):
-    """k_gmm_cov16 (default, 16x16x4 tiles) and the 32x32 fallback k_gmm_cov_async (2 (d=128) / 4
+    """k_gmm_cov16 (16x16x4 tiles), the bf16-part k_gmm_cov_bf3 (E^T E, E = sqrt(r) (x - m)) and
+    the 32x32 fallback k_gmm_cov_async (2 (d=128) / 4
     (d=64) components per workgroup, operands centred and weighted once per block into
     transposed LDS images, the same fp32 products): equal up to the order the MFMAs accumulate
     the samples in (atol 1e-5 of the matrix scale), symmetric (off-diagonal tiles are stored
@@ -281,10 +282,11 @@ def test_scatter_default_and_fallback_agree(V, K, d, chunks):
     resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
     mu = t(rng.standard_normal((K, d)).astype(np.float32))
     out = []
-    for opt in (3, 1):
+    for opt in (3, 1, 4):
         with opts(gmm_cov_async=opt):
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
-    np.testing.assert_allclose(out[1], out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
+    for o in out[1:]:
+        np.testing.assert_allclose(o, out[0], rtol=0, atol=1e-5 * np.abs(out[0]).max())
     for o in out:
         np.testing.assert_allclose(o, np.swapaxes(o, 1, 2), rtol=0, atol=1e-6 * np.abs(o).max())
 
