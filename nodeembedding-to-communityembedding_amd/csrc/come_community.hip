@@ -42,10 +42,6 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #ifndef COME_RESP_DIAG
 #define COME_RESP_DIAG 0
 #endif
-// k_community_bf3 A/B hook: N > 0 = explicit MFMA / N-VALU interleave per step (sched groups)
-#ifndef COME_BF3_SCHED
-#define COME_BF3_SCHED 0
-#endif
 // k_gmm_cov16 at d = 128: staging register sets (3 / 4 / 5+: 7.266 / 7.247 ms at C4 / spills)
 #ifndef COME_COV_NS
 #define COME_COV_NS 4
@@ -536,7 +532,10 @@ __global__ void __launch_bounds__(512, 4) k_community16(CommArgs a) {
 // + 7 of every step).  feat() orders the image rows so that accumulator register r of tile ct
 // belongs to the lane's own x[2 ct + r / 8][r % 8]: the update happens in registers.  M_k's image
 // is staged in quarters (2 k-steps, 24 KB at d = 128), two quarter buffers, one barrier per
-// quarter; quarter t + 2 is copied by LDS-DMA while t + 1 is multiplied.
+// quarter; quarter t + 2 is copied by LDS-DMA while t + 1 is multiplied.  (Measured and not
+// kept, profiles/r06_ab_community_bf3.txt: explicit MFMA / VALU sched groups; a sched_barrier-
+// pinned pipeline reading the next block's A parts into the registers each block frees and
+// splitting one B pair per block: 7.24 vs 7.16 ms; 8-wavefront workgroups, half-component units.)
 template <int D>
 struct CommBf3 {
     static constexpr int NS = D / 16;           // k-steps of 16 features
@@ -751,16 +750,6 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
                 }
 #pragma unroll
                 for (int P = 0; P < 3; ++P) Bc[P] = Bn[P];
-#if COME_BF3_SCHED
-                // A/B hook: interleave the next step's VALU with this step's MFMAs explicitly
-                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-                for (int i = 0; i < 6 * C::CT; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, COME_BF3_SCHED, 0);
-                    if (i % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
-#endif
             }
             if (t + 1 < nt) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1587,13 +1576,17 @@ struct RespBf3Shape {
     static constexpr int PIECES = UBYTES / 1024;
 };
 
-// the product shape: 4 wavefronts x 32 rows, four units of 5 blocks per component at d = 128
-// (4.65 / 4.68 ms vs 4.67 / 4.69 with two, profiles/r06_ab_estep_bf3.txt; A/B hooks below)
+// the product shape: 4 wavefronts x 32 rows, two units of 10 blocks per component at d = 128, A
+// parts read one block ahead (4.54 ms vs 4.58-4.61 with four units and no read-ahead,
+// profiles/r06_ab_estep_bf3.txt; A/B hooks below)
 #ifndef COME_RESP3_NW
 #define COME_RESP3_NW 4
 #endif
 #ifndef COME_RESP3_NU
-#define COME_RESP3_NU 4
+#define COME_RESP3_NU 2
+#endif
+#ifndef COME_RESP3_PF
+#define COME_RESP3_PF 1
 #endif
 template <int D>
 struct RespBf3Pick {
@@ -1708,6 +1701,65 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
         const float *par = reinterpret_cast<const float *>(smb + S::PAR) + (k & 1) * S::PARF;
         float sq = 0.0f;
         f32x16 acc[R::CT];
+        auto tile_sq = [&](int ct) {  // tile ct's squared residuals into sq
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const f32x4 mp = *reinterpret_cast<const f32x4 *>(par + 32 * ct + 8 * g4 + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float y = acc[ct][4 * g4 + e] - mp[e];
+                    sq = __builtin_fmaf(y, y, sq);
+                }
+            }
+        };
+#if COME_RESP3_PF
+        // A parts read one block ahead, each into the register its predecessor frees (A3 after
+        // the block's first MFMA, A2 after the third, A1 after the sixth), and a finished tile's
+        // squares taken after the next block's third MFMA (its accumulator is then complete
+        // and no MFMA of this wavefront waits on the VALU)
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int t = k * NU + u;
+            const char *ub = smb + (u & 1) * S::UBYTES;  // t & 1
+            auto ld = [&](int bi, int P) {
+                return *reinterpret_cast<const bf16x8 *>(ub + bi * R::BLK + aoff + P * 1024);
+            };
+            bf16x8 A[3];
+            A[2] = ld(0, 2);
+            A[1] = ld(0, 1);
+            A[0] = ld(0, 0);
+#pragma unroll
+            for (int bi = 0; bi < S::UB; ++bi) {
+                const int b = u * S::UB + bi, ct = TB.ct[b], s = TB.s[b];
+                const bool nx = bi + 1 < S::UB;
+                const f32x16 c0 = s == 0 ? f32x16{} : acc[ct];
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], xp[s][0], c0, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (nx) A[2] = ld(bi + 1, 2);
+                __builtin_amdgcn_sched_barrier(0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][0], acc[ct], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (nx) A[1] = ld(bi + 1, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][2], acc[ct], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (b > 0 && TB.s[b - 1] == 2 * TB.ct[b - 1] + 1) tile_sq(TB.ct[b - 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][0], acc[ct], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (nx) A[0] = ld(bi + 1, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (t + 1 < nt) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();  // buffer t & 1 free; unit t + 1 (and its parameters) in LDS
+                if (t + 2 < nt) respbf3_stage<D, NW, NU>(a, gimg, t + 2, smb, u & 1, wid, lane);
+            }
+        }
+        tile_sq(R::CT - 1);
+#else
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const int t = k * NU + u;
@@ -1727,18 +1779,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
                 acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][0], acc[ct], 0, 0, 0);
                 acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][1], acc[ct], 0, 0, 0);
                 acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][0], acc[ct], 0, 0, 0);
-                if (s == 2 * ct + 1) {  // tile ct complete
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const f32x4 mp =
-                            *reinterpret_cast<const f32x4 *>(par + 32 * ct + 8 * g4 + 4 * h);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const float y = acc[ct][4 * g4 + e] - mp[e];
-                            sq = __builtin_fmaf(y, y, sq);
-                        }
-                    }
-                }
+                if (s == 2 * ct + 1) tile_sq(ct);  // tile ct complete
             }
             if (t + 1 < nt) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1746,6 +1787,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
                 if (t + 2 < nt) respbf3_stage<D, NW, NU>(a, gimg, t + 2, smb, u & 1, wid, lane);
             }
         }
+#endif
         const float lp = par[256] - 0.5f * reduce_stage<5>(sq);
         lse_push(lp, run_max, run_sum);
         lp_prev = lp;
