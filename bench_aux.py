@@ -169,26 +169,27 @@ def c4(args):
                                     orc.precision_cholesky(cov), dev)
     flops = 2.0 * V * K * d * d
     # fraction of the MFMA blocks executed on sklearn's upper-triangular precision factors: the
-    # E-step's 16-wide blocks (k_gmm_resp16t, 36 of 64 at d = 128) or the fallback's 32-wide ones
-    # (k_gmm_resp_mfma, 10 of 16); the scatter's symmetric 16-wide (36 of 64) / 32-wide tiles
+    # bf16-part E-step's 32-wide column tiles x 16-feature steps (k_gmm_resp_bf3, 20 of 32 at
+    # d = 128) or the fp32 form's 16-wide blocks (k_gmm_resp16t, 36 of 64); the scatter's
+    # symmetric 32-wide (10 of 16, k_gmm_cov_bf3) / 16-wide (36 of 64, k_gmm_cov16) tiles
     from come_amd import _lib
     opts = _lib.launch_opts()
     ct = d // 32 if d in (64, 128) else 0
     tri = (ct * (ct + 1) / 2) / (ct * ct) if ct else 1.0
     ct16 = d // 16 if d in (64, 128) else 0
     tri16 = (ct16 * (ct16 + 1) / 2) / (ct16 * ct16) if ct16 else 1.0
-    tri_resp = (tri16 if opts.gmm_resp16 == 2 else
-                (ct * (ct + 1)) / (2 * ct * ct) if opts.gmm_resp16 == 3 else tri) if ct16 else 1.0
+    tri_resp = (tri16 if opts.gmm_resp16 == 2 else (ct * (ct + 1)) / (2 * ct * ct)) if ct16 \
+        else 1.0
     tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
-    cov_kernel = {1: "k_gmm_cov_async", 3: "k_gmm_cov16", 4: "k_gmm_cov_bf3"}[
+    cov_kernel = {3: "k_gmm_cov16", 4: "k_gmm_cov_bf3"}[
         opts.gmm_cov_async] if ct16 else "VALU"
-    comm_kernel = {1: "k_community_async", 2: "k_community16", 3: "k_community_bf3"}[
+    comm_kernel = {2: "k_community16", 3: "k_community_bf3"}[
         opts.community_async] if ct16 else "VALU"
     # k_community_bf3 carries each fp32 operand as three bf16 parts and takes six part products
     # per multiply-add: its ceiling is the bf16 MFMA peak / 6, not the fp32 MFMA peak
     comm_bf3 = comm_kernel == "k_community_bf3"
     comm_peak = BF16_MFMA_PEAK_TFLOPS / 6 if comm_bf3 else F32_MFMA_PEAK_TFLOPS
-    resp_kernel = {0: "k_gmm_resp_mfma", 2: "k_gmm_resp16t", 3: "k_gmm_resp_bf3"}[
+    resp_kernel = {2: "k_gmm_resp16t", 3: "k_gmm_resp_bf3"}[
         opts.gmm_resp16] if ct16 else "VALU"
     x0 = x.clone()
     xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]

@@ -34,8 +34,9 @@ extern "C" {
 #endif
 
 /* ABI 3 (this header): the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B
- * kernels) was removed, "community_async" accepts 1 / 2 / 3, "gmm_cov_async" 1 / 3 / 4 and "gmm_resp16"
- * 0 / 2 / 3 (other values: COME_E_INVALID at the call); come_source_sha256 was added.
+ * kernels) was removed, "community_async" accepts 2 / 3, "gmm_cov_async" 3 / 4 and "gmm_resp16"
+ * 2 / 3 (other values: COME_E_INVALID at the call; round 5 made the bf16-part kernels the
+ * defaults and removed the 32x32 fp32 fallbacks 1 / 1 / 0); come_source_sha256 was added.
  * ABI 2: come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
  * options "o2_plain_writeback" and "o2_pair_atomics" (ABI 1, ring-kernel Hogwild) were removed and
@@ -273,28 +274,25 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       VALU kernel): default 3 = k_community_bf3 (each fp32 operand as three
  *                       bf16 parts, six exact part products per multiply-add on 32x32x16 bf16
  *                       MFMAs -- fp32-level error, tests/test_gpu_c4.py; 7.3 vs 11.5 ms at C4);
- *                       2 = k_community16 (fp32 16x16x4 MFMAs, one 16-row tile per wavefront);
- *                       1 = the 32x32x2 fp32 fallback k_community_async.  Other values:
- *                       COME_E_INVALID
+ *                       2 = k_community16 (fp32 16x16x4 MFMAs, one 16-row tile per wavefront;
+ *                       11.5 ms).  Other values: COME_E_INVALID
  *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 4 = k_gmm_cov_bf3 (E^T E with
  *                       E = sqrt(r) (x - m) carried as three bf16 parts, six exact part products
  *                       per multiply-add on 32x32x16 bf16 MFMAs, 10 upper 32x32 tiles; 5.62 ms at
  *                       C4); 3 = k_gmm_cov16 (fp32 16x16x4 tiles: 36 of 64 upper tiles at d =
- *                       128; 7.22 ms); 1 = the 32x32 fp32 fallback k_gmm_cov_async (7.92 ms).
- *                       Other values: COME_E_INVALID
+ *                       128; 7.22 ms).  Other values: COME_E_INVALID
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
  *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
  *   gmm_resp16          GMM E-step at d = 64, 128: default 3 = k_gmm_resp_bf3 (fp32 operands
  *                       as three bf16 parts, six exact part products per multiply-add on 32x32x16
- *                       bf16 MFMAs, the row's parts formed once; 32-wide triangular skip; 4.65 ms
+ *                       bf16 MFMAs, the row's parts formed once; 32-wide triangular skip; 4.5 ms
  *                       at C4); 2 = k_gmm_resp16t on fp32 16x16x4 MFMAs (16-wide triangular skip,
  *                       in-lane row sums, the factors' non-zero 16x16 blocks packed, whole
  *                       components double-buffered, one barrier per component; 6.95 ms); a
  *                       launch holding a lower or dense factor runs every block, in
- *                       k_gmm_resp16_full, for both; 0 = the 32x32x2 fallback k_gmm_resp_mfma
- *                       (8.25 ms).  Other values: COME_E_INVALID
+ *                       k_gmm_resp16_full, for both.  Other values: COME_E_INVALID
  *   o1_chunk            O1: > 0 = one wavefront per chunk of that many consecutive edges, the
  *                       input row held in registers over each run of edges sharing it
  *                       (k_sgns_o1_runs); default -1 = one contiguous chunk per wavefront of the

@@ -179,177 +179,9 @@ __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
 // owns 128 rows; the `iters` loop runs in-kernel on the register-resident rows and x is written
 // back once.
 
-// ---- community gradient with asynchronous staging (d in {64, 128}) ----------------------------
-//
-// The 32x32 fallback (community_async = 1; the default is k_community16 below):
-// v_mfma_f32_32x32x2_f32 (64 cycles), lane (r, h) supplies A[row r][j] and B[j][col r] =
-// M_k[c0 + r][j], 4 wavefronts x 32 rows, CT = d/32 accumulator tiles each; the staging of M_{k+1}
-// overlaps the MFMAs of M_k (the E-step recipe):
-//  * k-step q, half-wave h uses element j(q, h) = 8 (q/4) + 4 h + q%4: four consecutive k-steps of
-//    a lane read one 16-B group g = 2 (q/4) + h of row c = ct*32 + r of M_k (one ds_read_b128).
-//  * The groups split into set A (g < NG/2, k-steps q < S/2) and set B (the rest).  Each set is
-//    its own LDS image of D rows x RL = NG/2 groups, groups XOR-swizzled per row so that a 16-lane
-//    group of the b128 read (16 different rows, one logical group) hits 16 different 16-B bank
-//    slots.  A set image is lane-linear in 1 KiB pieces, so global_load_lds_dwordx4 fills it with
-//    the swizzle applied on the SOURCE address.
-//  * After the barrier ending set A of component k, set A of M_{k+1}, mu_{k+1} (double-buffered)
-//    and pi[:, k+1] for the block's rows are copied while set B computes; set B of M_{k+1} follows
-//    after the next barrier.  Explicit vmcnt(0) before each barrier.
-template <int D>
-struct CommAsync {
-    static constexpr int S = D / 2, CT = D / 32, NG = D / 4, RL = NG / 2;
-    static constexpr int RPB = 16 / RL;              // rows per 256-B bank row in a set image
-    static constexpr int SET = D * RL * 4;           // floats per set image (= D*D/2)
-    static constexpr int MUS = D * D;                // 2 x 256 floats: mu_k, double-buffered
-    static constexpr int PIS = D * D + 512;          // 128 floats: pi[row, k] of the block's rows
-    static constexpr int LDX = D + 4;                // epilogue row tile stride
-    static constexpr int LDS_FLOATS = (PIS + 128) > 128 * LDX ? (PIS + 128) : 128 * LDX;
-    __device__ static int swz(int c) { return (c / RPB) & (RL - 1); }
-    // float offset of logical group g of row c
-    __device__ static int at(int c, int g) {
-        const int set = g / RL, gp = g % RL;
-        return set * SET + c * RL * 4 + ((gp ^ swz(c)) * 4);
-    }
-    __device__ static void stage_set(const float *Mk, float *sm, int set, int wid, int lane) {
-        constexpr int PIECES = SET / 256;
-        constexpr int ROWS = 256 / (RL * 4);          // rows per 1 KiB piece
-#pragma unroll
-        for (int i = wid; i < PIECES; i += 4) {
-            const int c = i * ROWS + lane / RL, pg = lane % RL;
-            const int g = set * RL + (pg ^ swz(c));
-            __builtin_amdgcn_global_load_lds(Mk + c * D + g * 4, sm + set * SET + i * 256, 16, 0,
-                                             0);
-        }
-    }
-    __device__ static void stage_mu(const float *mu, float *sm, int buf, int wid, int lane) {
-        if (wid == 0) {
-            const int src = lane * 4 < D ? lane * 4 : D - 4;
-            __builtin_amdgcn_global_load_lds(mu + src, sm + MUS + buf * 256, 16, 0, 0);
-        }
-    }
-    __device__ static void stage_pi(const CommArgs &a, int64_t blk0, int k, float *sm, int wid,
-                                    int lane) {
-        if (wid < 2) {
-            int64_t row = blk0 + wid * 64 + lane;
-            if (row >= a.V) row = a.V - 1;
-            __builtin_amdgcn_global_load_lds(a.pi + row * a.K + k, sm + PIS + wid * 64, 4, 0, 0);
-        }
-    }
-};
-
-template <int D, int M0, int M1>
-__device__ __forceinline__ void community_async_steps(
-    const float (&xa)[D / 2], const float *sm, const float *mus, float p, int h, int r,
-    __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
-    using C = CommAsync<D>;
-    float4 bq[C::CT], bn[C::CT];
-    float4 mq, mn;
-#pragma unroll
-    for (int ct = 0; ct < C::CT; ++ct)
-        bq[ct] = *reinterpret_cast<const float4 *>(sm + C::at(ct * 32 + r, 2 * M0 + h));
-    mq = *reinterpret_cast<const float4 *>(mus + 8 * M0 + 4 * h);
-#pragma unroll
-    for (int m = M0; m < M1; ++m) {
-        if (m + 1 < M1) {
-#pragma unroll
-            for (int ct = 0; ct < C::CT; ++ct)
-                bn[ct] = *reinterpret_cast<const float4 *>(sm + C::at(ct * 32 + r, 2 * (m + 1) + h));
-            mn = *reinterpret_cast<const float4 *>(mus + 8 * (m + 1) + 4 * h);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float av = p * (xa[4 * m + i] - mq[i]);
-#pragma unroll
-            for (int ct = 0; ct < C::CT; ++ct)
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq[ct][i], acc[ct], 0, 0, 0);
-        }
-        if (m + 1 < M1) {
-#pragma unroll
-            for (int ct = 0; ct < C::CT; ++ct) bq[ct] = bn[ct];
-            mq = mn;
-        }
-    }
-}
-
-template <int D>
-__global__ void __launch_bounds__(256, 2) k_community_async(CommArgs a) {
-    using C = CommAsync<D>;
-    constexpr int S = C::S, CT = C::CT, LDX = C::LDX;
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int tid = threadIdx.x;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t blk0 = (int64_t)blockIdx.x * 128;
-    const int64_t myrow = blk0 + wid * 32 + r;
-    const bool rowok = myrow < a.V;
-    auto jcol = [&](int q) { return 8 * (q / 4) + 4 * h + (q % 4); };
-    float xa[S];
-#pragma unroll
-    for (int q = 0; q < S; ++q) xa[q] = rowok ? a.x[myrow * D + jcol(q)] : 0.0f;
-
-    for (int it = 0; it < a.iters; ++it) {
-        __syncthreads();  // the previous epilogue's row tile is free
-        C::stage_set(a.inv_cov, sm, 0, wid, lane);
-        C::stage_set(a.inv_cov, sm, 1, wid, lane);
-        C::stage_mu(a.mu, sm, 0, wid, lane);
-        C::stage_pi(a, blk0, 0, sm, wid, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        f32x16 acc[CT];
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-        for (int k = 0; k < a.K; ++k) {
-            const float p = sm[C::PIS + wid * 32 + r];
-            const float *mus = sm + C::MUS + (k & 1) * 256;
-            const float *Mn = a.inv_cov + (int64_t)(k + 1) * D * D;
-            community_async_steps<D, 0, S / 8>(xa, sm, mus, p, h, r, acc);  // set A of M_k
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // set A and pi free; set B of M_k in LDS
-            if (k + 1 < a.K) {
-                C::stage_set(Mn, sm, 0, wid, lane);
-                C::stage_mu(a.mu + (int64_t)(k + 1) * D, sm, (k + 1) & 1, wid, lane);
-                C::stage_pi(a, blk0, k + 1, sm, wid, lane);
-            }
-            community_async_steps<D, S / 8, S / 4>(xa, sm, mus, p, h, r, acc);  // set B of M_k
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // set B free; set A, mu and pi of k+1 in LDS
-            if (k + 1 < a.K) C::stage_set(Mn, sm, 1, wid, lane);
-        }
-        // epilogue: x -= lr * clip(coef * G, -5, 5), through a [128][LDX] LDS row tile (no copy
-        // is in flight: the last component issues none)
-        float *X = sm + wid * 32 * LDX;  // this wavefront's 32 rows
-#pragma unroll
-        for (int q = 0; q < S; ++q) X[r * LDX + jcol(q)] = xa[q];
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's rows are in LDS
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-                float *px = X + row * LDX + ct * 32 + r;
-                float g = acc[ct][e] * a.coef;
-                g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);
-                *px = *px - g * a.lr;
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < S; ++q) xa[q] = X[r * LDX + jcol(q)];
-    }
-    if (rowok) {
-#pragma unroll
-        for (int q = 0; q < S; ++q) a.x[myrow * D + jcol(q)] = xa[q];
-    }
-}
-
 // ---- community gradient on 16x16x4 MFMAs, one 16-row tile per wavefront (community_async = 2) --
 //
-// k_community_async's staging (two half images of M_k = Sigma_k^-1, set A = columns s < D/2 and
+// Staging in two half images of M_k = Sigma_k^-1 (set A = columns s < D/2 and
 // set B = the rest, each half staged while the other is multiplied; mu_k double-buffered), with
 // the E-step's wave shape: 8 wavefronts x 16 rows per 128-row workgroup, about 90 VGPRs, so the
 // two workgroups the LDS holds per CU give 4 waves per SIMD instead of 2.  MFMA (column tile ct,
@@ -787,34 +619,12 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     }
 }
 
-// GMM responsibilities on MFMA (d in {64, 128}): for each component the tile computes
-// Y = X P_k (A = the rows, B = P_k), then sum_c (Y - mu P_k)^2 per row: squares summed over the CT
-// column tiles in registers, then over the 32 columns of a half-wave with the DPP / permlane16
-// stages 0-4.  Per-component log-probabilities go to resp_out itself (scratch, one row per lane
-// group), the softmax over k finishes in place.
-//
-// Operand layout: the k-steps pair feature indices s(g, i, h) = 8 g + 4 h + i (group g of four
-// k-steps), so a lane's four consecutive k-steps use four consecutive features: A comes from one
-// float4 of the row held in registers, B from one ds_read_b128 of P_k^T (rows = output columns c,
-// 4 consecutive s) -- one LDS instruction per 4 MFMAs per column tile instead of one per MFMA, and
-// group g + 1's B operands are read while group g's MFMAs run.  P^T (k_transpose_sq, once per
-// call) is staged into two half images (s < D/2, s >= D/2), rows padded to D/2 + 4 floats so the
-// 16 lanes of each b128 phase hit 16 distinct 4-bank groups.
-//
-// Triangular skip: sklearn's precisions_cholesky_ after an M-step is UPPER triangular
-// (solve_triangular(chol(cov), I, lower=True).T), so column tile ct only needs features s <= 32 ct
-// + 31 of P_k, i.e. groups g < 4 (ct + 1): 10 of the 16 32x32 blocks at d = 128 (0.625 of the
-// MFMAs).  k_gmm_lower_flags marks the components with a non-zero below the diagonal (a lower
-// factor, e.g. sklearn's cholesky(precisions_init, lower=True)); those run the full loop.  The
-// skipped MFMAs would only add exact zeros, so both paths give identical results.
-//
-// Staging is asynchronous: groups g < D/16 read only half image A, the others half image B.
-// After every wavefront has finished half A of component k (barrier), half A of P_{k+1}^T is copied
-// global -> LDS by global_load_lds_dwordx4 (1 KiB per wave instruction; each lane computes its own
-// source so the LDS image comes out padded) while the half-B MFMAs and the epilogue of k run; half
-// B and mu_{k+1} P_{k+1} follow after the next barrier, in flight during the next half A.  Each
-// barrier is a plain __syncthreads (its vmcnt(0) retires exactly the copies the next phase reads).
-// No VGPRs are spent on staging.
+// GMM responsibilities, shared steps.  Triangular skip: sklearn's precisions_cholesky_ after an
+// M-step is UPPER triangular (solve_triangular(chol(cov), I, lower=True).T), so a column tile of
+// Y = X P_k only needs the features up to its last column.  k_gmm_lower_flags marks the components
+// with a non-zero below the diagonal (a lower factor, e.g. sklearn's cholesky(precisions_init,
+// lower=True)) and ORs them into flags[K]; a launch holding one runs the full-body kernel
+// (k_gmm_resp16_full) instead of the skipping one.  The skipped MFMAs would only add exact zeros.
 __global__ void __launch_bounds__(256) k_gmm_lower_flags(const float *__restrict__ P, int D,
                                                          int *__restrict__ flags, int K) {
     const float *Pk = P + (int64_t)blockIdx.x * D * D;
@@ -841,205 +651,6 @@ __global__ void __launch_bounds__(256) k_transpose_sq(const float *__restrict__ 
     for (int y = y0; y < 32; y += 8) dst[(int64_t)(tc * 32 + y) * D + tr * 32 + x] = t[x][y];
 }
 
-template <int D>
-struct RespShape {
-    static constexpr int CT = D / 32;
-    static constexpr int G = D / 8;            // k-step groups
-    static constexpr int HLD = D / 2 + 4;      // padded row of a half image
-    static constexpr int HIMG = D * HLD;       // floats per half image
-    static constexpr int MP = 2 * HIMG;        // mu_k P_k (D floats, 256 reserved)
-    static constexpr int PARAMS = MP + 256;    // lower flag, log_norm (64 reserved)
-    static constexpr int LDS = PARAMS + 64;    // floats
-    static_assert(HIMG % 256 == 0, "a half image is a whole number of 1 KiB copies");
-};
-
-// groups [G0, G1) of one component: B operands of group g + 1 read while group g computes
-template <int D, int G0, int G1>
-__device__ __forceinline__ void resp_mfma_groups(
-    const __attribute__((ext_vector_type(4))) float (&xa)[D / 8], const float *sm, int h, int r,
-    bool full, __attribute__((ext_vector_type(16))) float (&acc)[D / 32]) {
-    using RS = RespShape<D>;
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int CT = RS::CT;
-    auto fetch = [&](int g, f32x4 (&bv)[CT]) {
-        const float *img = sm + (g < RS::G / 2 ? 0 : RS::HIMG);
-        const int s0 = 8 * g - (g < RS::G / 2 ? 0 : D / 2) + 4 * h;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-            bv[ct] = *reinterpret_cast<const f32x4 *>(img + (ct * 32 + r) * RS::HLD + s0);
-    };
-    f32x4 bv[2][CT];
-    fetch(G0, bv[0]);
-#pragma unroll
-    for (int g = G0; g < G1; ++g) {
-        const int cur = (g - G0) & 1;
-        if (g + 1 < G1) fetch(g + 1, bv[cur ^ 1]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                if (g >= 4 * (ct + 1) && !full) continue;
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[g][i], bv[cur][ct][i], acc[ct],
-                                                               0, 0, 0);
-            }
-    }
-}
-
-// copy half image `half` of P_k^T (rows c, features [half D/2, half D/2 + D/2), padded rows) into
-// LDS; wavefront wid of 4, 1 KiB per instruction; padding lanes re-read a valid address
-template <int D>
-__device__ __forceinline__ void resp_stage_half(const float *Ptk, float *sm, int half, int wid,
-                                                int lane) {
-    using RS = RespShape<D>;
-    constexpr int PIECES = RS::HIMG / 256;
-#pragma unroll
-    for (int j = 0; j < (PIECES + 3) / 4; ++j) {
-        const int i = wid + 4 * j;
-        if (i >= PIECES) break;  // wavefront-uniform
-        const int o = i * 256 + lane * 4;
-        const int c = o / RS::HLD, s = o % RS::HLD;
-        const int sc = s < D / 2 ? s : D / 2 - 4;
-        __builtin_amdgcn_global_load_lds(Ptk + c * D + half * (D / 2) + sc,
-                                         sm + half * RS::HIMG + i * 256, 16, 0, 0);
-    }
-}
-
-// mu_k P_k (D floats) into sm[MP .. MP + 256): wavefront 0, lanes past D/4 re-read the last
-// 16 B (their copies land in the unused tail of the 1 KiB region)
-template <int D>
-__device__ __forceinline__ void resp_stage_mp(const float *mp, float *sm, int wid, int lane) {
-    if (wid == 0) {
-        const int src = lane * 4 < D ? lane * 4 : D - 4;
-        __builtin_amdgcn_global_load_lds(mp + src, sm + RespShape<D>::MP, 16, 0, 0);
-    }
-}
-
-// lower[k] and log_norm[k] into sm[PARAMS ..]: lanes 0 and 1 of wavefront 0 (a vector load of
-// them would make the compiler wait vmcnt(0) at their first use -- draining the copies in flight;
-// loaded from LDS after the barrier instead)
-template <int D>
-__device__ __forceinline__ void resp_stage_params(const RespArgs &a, int k, float *sm, int wid,
-                                                  int lane) {
-    if (wid == 0) {
-        const float *src = lane == 0 ? reinterpret_cast<const float *>(a.lower + k)
-                                     : a.log_norm + k;
-        __builtin_amdgcn_global_load_lds(src, sm + RespShape<D>::PARAMS, 4, 0, 0);
-    }
-}
-
-template <int D>
-__global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
-    using RS = RespShape<D>;
-    constexpr int CT = RS::CT;
-    constexpr int G = RS::G;
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const float *mps = sm + RS::MP;
-    const int tid = threadIdx.x;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t blk0 = (int64_t)blockIdx.x * 128;
-    const int64_t myrow = blk0 + wid * 32 + r;
-    const bool rowok = myrow < a.V;
-    f32x4 xa[G];  // xa[g][i] = x[row][8 g + 4 h + i]
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        xa[g] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (rowok) xa[g] = *reinterpret_cast<const f32x4 *>(a.x + myrow * D + 8 * g + 4 * h);
-    }
-    resp_stage_half<D>(a.prec_t, sm, 0, wid, lane);
-    resp_stage_half<D>(a.prec_t, sm, 1, wid, lane);
-    resp_stage_mp<D>(a.mu_prec, sm, wid, lane);
-    resp_stage_params<D>(a, 0, sm, wid, lane);
-    __syncthreads();
-    // the row this lane's reduce-scatter ends on (lanes r < 16 of each half-wave; see below)
-    const int my_e = 8 * ((r >> 3) & 1) + 4 * ((r >> 2) & 1) + 2 * (r & 1) + ((r >> 1) & 1);
-    const int64_t my_row = blk0 + wid * 32 + (my_e & 3) + 8 * (my_e >> 2) + 4 * h;
-    float run_max = -INFINITY, run_sum = 0.0f;
-    for (int k = 0; k < a.K; ++k) {
-        const float *pr = sm + RS::PARAMS;
-        const bool full = __builtin_amdgcn_readfirstlane(__float_as_int(pr[0])) != 0;
-        const float lnk = pr[1];
-        const float *Pn = a.prec_t + (int64_t)(k + 1) * D * D;
-        f32x16 acc[CT];
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-        resp_mfma_groups<D, 0, G / 2>(xa, sm, h, r, full, acc);
-        // the copies issued before the loop back-edge are not tracked by the compiler's barrier
-        // fence (it emitted no vmcnt wait here): retire them explicitly before the barrier
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // half A of P_k and the params free; half B and mu_k P_k in LDS
-        if (k + 1 < a.K) {
-            resp_stage_half<D>(Pn, sm, 0, wid, lane);
-            resp_stage_params<D>(a, k + 1, sm, wid, lane);
-        }
-        resp_mfma_groups<D, G / 2, G>(xa, sm, h, r, full, acc);
-        float sq[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            sq[e] = 0.0f;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const float y = acc[ct][e] - mps[ct * 32 + r];
-                sq[e] = __builtin_fmaf(y, y, sq[e]);
-            }
-        }
-        // Sum over the 32 columns r of a half-wave for each of its 16 rows e: a reduce-scatter
-        // butterfly (each stage keeps half of the values and adds the partner's copy of them), so
-        // lane r ends with row e(r) = 8 b3 + 4 b2 + 2 b0 + b1 (b = bits of r) after 8+4+2+1 DPP
-        // adds + one permlane16 add, and the wave stores all 32 rows of the tile at once.  The
-        // partners are mirrors first (they flip the lower bits too, so they must come before
-        // the quad stages): row_mirror (bit 3), row_half_mirror (bit 2), then quad xor 1 and 2.
-        const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
-        auto scatter_stage = [](float *v, int n, int keep_hi, auto partner) {
-#pragma unroll
-            for (int i = 0; i < n; ++i) {
-                const float keep = keep_hi ? v[i + n] : v[i];
-                const float send = keep_hi ? v[i] : v[i + n];
-                v[i] = keep + partner(send);
-            }
-        };
-        auto dpp = [](float x, auto ctrl) {
-            return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
-                                                              decltype(ctrl)::value, 0xF, 0xF,
-                                                              false));
-        };
-        scatter_stage(sq, 8, b3, [&](float x) { return dpp(x, std::integral_constant<int, 0x140>{}); });
-        scatter_stage(sq, 4, b2, [&](float x) { return dpp(x, std::integral_constant<int, 0x141>{}); });
-        scatter_stage(sq, 2, b0, [&](float x) { return dpp(x, std::integral_constant<int, 0xB1>{}); });
-        scatter_stage(sq, 1, b1, [&](float x) { return dpp(x, std::integral_constant<int, 0x4E>{}); });
-        const float tot = reduce_stage<4>(sq[0]);  // + the other 16 columns (lane r ^ 16)
-        {
-            const float lp = lnk - 0.5f * tot;
-            if (r < 16 && my_row < a.V) a.resp[my_row * a.K + k] = lp;
-            // online log-sum-exp of the row's components so far
-            if (lp > run_max) {
-                run_sum = run_sum * expf(run_max - lp) + 1.0f;
-                run_max = lp;
-            } else {
-                run_sum += expf(lp - run_max);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // half B of P_k and mu_k P_k free; half A of P_{k+1} in LDS
-        if (k + 1 < a.K) {
-            resp_stage_half<D>(Pn, sm, 1, wid, lane);
-            resp_stage_mp<D>(a.mu_prec + (int64_t)(k + 1) * D, sm, wid, lane);
-        }
-    }
-    // softmax over k in place: the lane that wrote the row's log-probabilities normalises them
-    // (one read-write pass; max and sum were kept online)
-    if (r < 16 && my_row < a.V) {
-        float *lp = a.resp + my_row * a.K;
-        const float lse = run_max + logf(run_sum);
-        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
-        if (a.lse) a.lse[my_row] = lse;
-    }
-}
-
 // ---- E-step on v_mfma_f32_16x16x4_f32: the FULL body (k_gmm_resp16_full) ------------------
 //
 // Y^T = P_k^T X^T per 16 x 16 tile: A = P_k^T (lane: column c = ct*16 + lane%16, features
@@ -1050,14 +661,14 @@ __global__ void __launch_bounds__(256, 2) k_gmm_resp_mfma(RespArgs a) {
 // 4 x CT values plus two cross-lane adds (lane ^ 16, lane ^ 32) -- no reduce-scatter.
 // 16-wide blocks skip more of sklearn's upper precision factor than 32-wide ones: block (quad q,
 // column tile ct) is non-zero iff q <= ct, 36 of 64 blocks at d = 128 (0.5625 of the dense MFMA
-// cycles; k_gmm_resp_mfma: 10 of 16 32-wide blocks = 0.625), at the same fp32 rate (32 cycles per
+// cycles; 32-wide blocks: 10 of 16 = 0.625), at the same fp32 rate (32 cycles per
 // 16x16x4 MFMA = 64 per 32x32x2, half the flops).
 // A workgroup = 4 wavefronts x 32 rows (RT = 2 row tiles), two workgroups per CU.  P_k^T lives in
 // LDS as two half images of D rows x D/2 features; half 0 holds quads {0 .. NQ/4-1} and
 // {3NQ/4 .. NQ-1}, half 1 the middle ones, so both phases of a component run the same number of
-// MFMAs (18 + 18 (quad, tile) blocks at d = 128; k_gmm_resp_mfma's halves: 112 vs 48 MFMAs).
+// MFMAs (18 + 18 (quad, tile) blocks at d = 128; a plain split of the features: 112 vs 48 MFMAs).
 // The next component's half is copied global -> LDS (global_load_lds) while the other half
-// computes, as in k_gmm_resp_mfma.  Rows of an image are 16-B granules XOR-swizzled by the row
+// computes.  Rows of an image are 16-B granules XOR-swizzled by the row
 // (granule g of row r at g ^ (r % granules)): conflict-free ds_read_b128 without padding.
 template <int D>
 struct Resp16Shape {
@@ -1836,308 +1447,11 @@ struct CovArgs {
     int K;
 };
 
-// Symmetric output: only the CT (CT + 1) / 2 tiles with rt <= ct are accumulated (10 of 16 at
-// d = 128, 3 of 4 at d = 64), and each off-diagonal tile is also stored transposed -- S_k comes out
-// exactly symmetric.
-template <int D>
-struct CovShape {
-    static constexpr int CT = D / 32;
-    static constexpr int NT = CT * (CT + 1) / 2;
-    // k_gmm_cov_async: CPW components per workgroup, 4 MFMA wavefronts (one per SIMD) with ATPW
-    // tiles each -- the CPW * NT tiles split evenly (2 x 10 = 4 x 5 at d = 128, 4 x 3 = 4 x 3 at
-    // 64) -- plus 4 staging wavefronts
-    static constexpr int AWAVES = 4;
-    static constexpr int ATHREADS = 2 * 64 * AWAVES;
-    static constexpr int CPW = D == 128 ? 2 : 4;
-    static constexpr int ATPW = CPW * NT / AWAVES;
-    static_assert(CPW * NT % AWAVES == 0, "async tiles must split evenly");
-};
-
-// tile t of the upper triangle (row-major over rt <= ct) -> (rt, ct)
-__device__ __forceinline__ void upper_tile(int t, int CT, int &rt, int &ct) {
-    rt = 0;
-    while (t >= CT - rt) {
-        t -= CT - rt;
-        ++rt;
-    }
-    ct = rt + t;
-}
-
-// The upper tiles T0 .. T0 + ATPW - 1 of one component (one MFMA wavefront's share), with the
-// distinct A-row and B-column tile indices they read, all at compile time.
-template <int D, int T0>
-struct CovTiles {
-    static constexpr int CT = CovShape<D>::CT;
-    static constexpr int N = CovShape<D>::ATPW;
-    static constexpr int rt(int t) {
-        int f = T0 + t, r = 0;
-        while (f >= CT - r) {
-            f -= CT - r;
-            ++r;
-        }
-        return r;
-    }
-    static constexpr int ct(int t) {
-        int f = T0 + t, r = 0;
-        while (f >= CT - r) {
-            f -= CT - r;
-            ++r;
-        }
-        return r + f;
-    }
-    // distinct values of rt (A) / ct (B) in order of first use; idx = position of tile t's
-    template <bool A>
-    static constexpr int val(int t) { return A ? rt(t) : ct(t); }
-    template <bool A>
-    static constexpr int count() {
-        int n = 0;
-        for (int t = 0; t < N; ++t) {
-            bool seen = false;
-            for (int u = 0; u < t; ++u) seen = seen || val<A>(u) == val<A>(t);
-            n += seen ? 0 : 1;
-        }
-        return n;
-    }
-    template <bool A>
-    static constexpr int nth(int i) {
-        int n = 0;
-        for (int t = 0; t < N; ++t) {
-            bool seen = false;
-            for (int u = 0; u < t; ++u) seen = seen || val<A>(u) == val<A>(t);
-            if (!seen) {
-                if (n == i) return val<A>(t);
-                ++n;
-            }
-        }
-        return -1;
-    }
-    template <bool A>
-    static constexpr int idx(int t) {
-        for (int i = 0; i < count<A>(); ++i)
-            if (nth<A>(i) == val<A>(t)) return i;
-        return -1;
-    }
-    struct Table {
-        int v[N];
-    };
-    template <bool A>
-    static constexpr Table idx_table() {
-        Table r{};
-        for (int t = 0; t < N; ++t) r.v[t] = idx<A>(t);
-        return r;
-    }
-};
-
-// Two image buffers, two workgroups per CU (<= 128 registers per wavefront): the other
-// workgroup's MFMA wavefront covers each one's barrier.  (Three buffers and one workgroup per CU,
-// reading the next block's first operands before its barrier: 8.7 vs 7.9 ms at C4.)
-template <int D>
-struct CovAsync {
-    static constexpr int RB = 32;                         // samples per block
-    static constexpr int LDT = RB + 4;                    // padded row of a transposed image
-    static constexpr int IMG = D * LDT;                   // floats per image
-    static constexpr int CPW = CovShape<D>::CPW;
-    static constexpr int WOFF = CPW * IMG;                // weights [CPW][RB] after the images
-    static constexpr int BUF = CPW * IMG + CPW * RB;      // floats per buffer
-    static constexpr int NBUF = 2;
-    static constexpr int WPE = 4;                         // waves per SIMD the kernel is built for
-};
-
-// One MFMA wavefront over all nb blocks: one operand register set, group g + 1's operands read
-// after group g's MFMAs are issued.
-template <int D, int T0>
-__device__ __forceinline__ void cov_consume(const float *img, int nb, int tk, int lane,
-                                            __attribute__((ext_vector_type(16)))
-                                            float (&acc)[CovShape<D>::ATPW]) {
-    using TS = CovTiles<D, T0>;
-    using CA = CovAsync<D>;
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int N = TS::N;
-    constexpr int NA = TS::template count<true>();
-    constexpr int NB = TS::template count<false>();
-    const int r = lane & 31, h = lane >> 5;
-    int ab[NA], bb[NB];
-#pragma unroll
-    for (int i = 0; i < NA; ++i)
-        ab[i] = tk * CA::IMG + (TS::template nth<true>(i) * 32 + r) * CA::LDT + 4 * h;
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-        bb[i] = tk * CA::IMG + (TS::template nth<false>(i) * 32 + r) * CA::LDT + 4 * h;
-    const int wb = CA::WOFF + tk * CA::RB + 4 * h;
-    constexpr typename TS::Table IA = TS::template idx_table<true>();
-    constexpr typename TS::Table IB = TS::template idx_table<false>();
-    f32x4 ra[NA], rb[NB], rw;
-    auto fetch = [&](int blk, int g) {
-        const float *buf = img + (blk % CA::NBUF) * CA::BUF + 8 * g;
-#pragma unroll
-        for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const f32x4 *>(buf + ab[i]);
-#pragma unroll
-        for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const f32x4 *>(buf + bb[i]);
-        rw = *reinterpret_cast<const f32x4 *>(buf + wb);
-    };
-    for (int j = 0; j < nb; ++j) {
-        __syncthreads();  // barrier j: block j staged
-        fetch(j, 0);
-#pragma unroll
-        for (int g = 0; g < CA::RB / 8; ++g) {
-            f32x4 wa[NA];  // A = r * (x - mu): every MFMA operand an exact fp32 product
-#pragma unroll
-            for (int i = 0; i < NA; ++i) wa[i] = rw * ra[i];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int t = 0; t < N; ++t)
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                        wa[IA.v[t]][q], rb[IB.v[t]][q], acc[t], 0, 0, 0);
-            if (g + 1 < CA::RB / 8) fetch(j, g + 1);
-        }
-    }
-}
-
-// The 32x32 fallback (gmm_cov_async = 1; the default is k_gmm_cov16 below).  What limited the
-// earlier forms (SQ counters at C4, profiles/r01h_c4_pmc_sq.txt, profiles/r02_c4_scatter_ab.txt):
-// VALU work per MFMA (every operand centred and weighted at read time: 8.6 VALU per MFMA), SIMD
-// imbalance (5-wavefront workgroups put two tile sets on one SIMD of four), MFMA wavefronts
-// stopping to stage each block, and sample loads landing later than one block period.  Here:
-//  * CPW components per workgroup (2 at d = 128, 4 at d = 64): the CPW x NT upper tiles split
-//    exactly over 4 MFMA wavefronts (ATPW each, one per SIMD), and the components share one
-//    global read of each sample block;
-//  * 4 more wavefronts only stage: a 32-sample block is loaded global -> VGPRs three blocks
-//    ahead, centred once per component into a transposed LDS image B[k][c][s] = x_s[c] - mu_k[c]
-//    (rows padded to 36 floats) and its weights r_sk stored beside it.  The MFMA wavefronts form
-//    A = r_sk * B[k][c][s] in registers (the synchronous form's fp32 subtraction and product:
-//    every MFMA operand is bit-identical), 4 VALU per distinct A row per 20 MFMAs;
-//  * two image buffers: block j + 1 is staged while block j is multiplied, 74 KB, two workgroups
-//    per CU whose MFMA wavefronts cover each other's barriers; one barrier per block;
-//  * the k-steps pair samples s(q, h) = 8 (q/4) + 4 h + q%4, so the four consecutive k-steps of
-//    a lane read one 16-byte group of a row: one ds_read_b128 per distinct operand row per 4
-//    MFMAs (6 or 5 rows for a wavefront's 5 tiles at d = 128), and the padding sends the 16
-//    lanes of each b128 phase to 16 distinct 4-bank groups.
-// C4 (V = 1M, K = 50, d = 128): 7.9 ms vs 11.3 ms for round 1's synchronous form.
-template <int D>
-__global__ void __launch_bounds__(CovShape<D>::ATHREADS)
-    __attribute__((amdgpu_waves_per_eu(CovAsync<D>::WPE))) k_gmm_cov_async(CovArgs a) {
-    using CA = CovAsync<D>;
-    constexpr int NT = CovShape<D>::NT;
-    constexpr int CPW = CA::CPW;
-    constexpr int TPW = CovShape<D>::ATPW;
-    constexpr int NST = 64 * CovShape<D>::AWAVES;  // staging threads
-    constexpr int RB = CA::RB;
-    constexpr int SPT = RB * D / NST;  // samples staged per thread (16 at d = 128, 8 at d = 64)
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    static_assert(SPT % 4 == 0 && SPT * CPW <= 64 && D % 64 == 0, "staging layout");
-    static_assert(CA::NBUF * CA::BUF * sizeof(float) <= 160 * 1024, "LDS budget");
-    static_assert(TPW <= NT && NT % TPW == 0, "a wavefront's tiles lie in one component");
-    __shared__ __attribute__((aligned(16))) float img[CA::NBUF * CA::BUF];
-    const int k0 = blockIdx.x * CPW;
-    const int nk = a.K - k0 < CPW ? a.K - k0 : CPW;
-    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
-    int64_t c1 = c0 + a.rows_per_chunk;
-    if (c1 > a.V) c1 = a.V;
-    const int nb = c1 > c0 ? (int)((c1 - c0 + RB - 1) / RB) : 0;
-    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    if (wid < CovShape<D>::AWAVES) {
-        // ---- MFMA wavefronts: component tk, tiles t0 .. t0 + TPW - 1 ----
-        const int tk = wid * TPW / NT, t0 = wid * TPW % NT;
-        f32x16 acc[TPW];
-#pragma unroll
-        for (int t = 0; t < TPW; ++t)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
-        if (nb > 0) {
-            if (t0 == 0) cov_consume<D, 0>(img, nb, tk, lane, acc);
-            else cov_consume<D, (NT == TPW ? 0 : TPW)>(img, nb, tk, lane, acc);
-        }
-        if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
-        const int r = lane & 31, h = lane >> 5;
-        float *out = a.out + ((int64_t)blockIdx.y * a.K + k0 + tk) * D * D;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            int rt, ct;
-            upper_tile(t0 + t, CovShape<D>::CT, rt, ct);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int ii = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                const int jj = ct * 32 + r;
-                out[(int64_t)ii * D + jj] = acc[t][e];
-                if (rt != ct) out[(int64_t)jj * D + ii] = acc[t][e];
-            }
-        }
-        return;
-    }
-    // ---- staging wavefronts: thread owns column sc and samples SPT sp .. SPT sp + SPT - 1 of a
-    // block (sp uniform over a wavefront); lane l < SPT * CPW also carries the weight of sample
-    // SPT sp + l % SPT for component k0 + l / SPT ----
-    const int st = tid - NST;
-    const int sc = st % D, sp = st / D;
-    float mu[CPW];
-#pragma unroll
-    for (int kk = 0; kk < CPW; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
-    // block b's samples and weight live in register set b % 3: loads run 3 blocks ahead of the
-    // stage that consumes them (an HBM / MALL round trip under load exceeds one block period)
-    float xv[3][SPT];
-    float wl[3];
-    const int wk = lane / SPT, ws = lane % SPT;
-    const bool wlane = lane < SPT * CPW;
-    auto load = [&](int blk, float (&xr)[SPT], float &wr) {
-        const int64_t b = c0 + (int64_t)blk * RB;
-        const float *src = a.x + (b + SPT * sp) * D + sc;
-        if (b + RB <= c1) {
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) xr[q] = src[q * D];
-        } else {
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) xr[q] = b + SPT * sp + q < c1 ? src[q * D] : 0.0f;
-        }
-        const int64_t wrow = b + SPT * sp + ws;
-        wr = wlane && wk < nk && wrow < c1 ? a.resp[wrow * a.K + k0 + wk] : 0.0f;
-    };
-    auto stage = [&](int blk, const float (&xr)[SPT], float wr) {
-        float *buf = img + (blk % CA::NBUF) * CA::BUF;
-#pragma unroll
-        for (int kk = 0; kk < CPW; ++kk)
-#pragma unroll
-            for (int j = 0; j < SPT / 4; ++j) {
-                f32x4 xb;
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) xb[q4] = xr[4 * j + q4] - mu[kk];
-                *reinterpret_cast<f32x4 *>(buf + kk * CA::IMG + sc * CA::LDT + SPT * sp + 4 * j) =
-                    xb;
-            }
-        if (wlane) buf[CA::WOFF + wk * RB + SPT * sp + ws] = wr;
-    };
-    if (nb == 0) return;
-    constexpr int SD = CA::NBUF - 1;  // block j + SD is staged while block j is multiplied
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-        if (u < nb) load(u, xv[u], wl[u]);
-#pragma unroll
-    for (int u = 0; u < SD; ++u)
-        if (u < nb) {
-            stage(u, xv[u], wl[u]);
-            if (u + 3 < nb) load(u + 3, xv[u], wl[u]);
-        }
-    __syncthreads();  // barrier 0
-    for (int j0 = 0; j0 < nb; j0 += 3) {
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {  // j = j0 + u, j0 % 3 == 0: register set (j + SD) % 3
-            const int j = j0 + u;
-            if (j >= nb) break;
-            if (j + SD < nb) {
-                // buffer (j + SD) % NBUF = (j - 1) % NBUF: block j - 1 finished at barrier j
-                stage(j + SD, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-                if (j + SD + 3 < nb) load(j + SD + 3, xv[(u + SD) % 3], wl[(u + SD) % 3]);
-            }
-            if (j + 1 < nb) __syncthreads();  // barrier j + 1
-        }
-    }
-}
-
 // ---- M-step scatter on v_mfma_f32_16x16x4_f32 (k_gmm_cov16, gmm_cov_async = 3) ----------------
 //
-// k_gmm_cov_async's structure (4 MFMA + 4 staging wavefronts, CPW components per workgroup, two
-// image buffers, two workgroups per CU) on 16 x 16 output tiles: the symmetric output needs the
+// 4 MFMA + 4 staging wavefronts, CPW components per workgroup, two image buffers, two workgroups
+// per CU, on 16 x 16 output tiles (only rt <= ct; each off-diagonal tile also stored transposed,
+// so S_k comes out exactly symmetric): the symmetric output needs the
 // 36 upper tiles of 64 at d = 128 (0.5625 of the dense MFMA cycles) instead of 10 of 16 32-wide
 // tiles (0.625).  MFMA (tile rt, ct; 4 samples): A[i][k] = w_s (x_s - mu)[rt*16 + i], B[k][j] =
 // (x_s - mu)[ct*16 + j], lane l: i = j = l % 16, samples s = 16 g + 4 (l / 16) + t for the four
@@ -2341,7 +1655,7 @@ struct Cov16StageX4 {
     }
 };
 
-// d = 64 (and k_gmm_cov_async's layout): thread owns column sc and samples SPT sp .. SPT sp + SPT
+// d = 64: thread owns column sc and samples SPT sp .. SPT sp + SPT
 // - 1 of a block; lane l also carries the weight of sample SPT sp + l % SPT for component
 // l % (SPT CPW) / SPT
 template <int D>
@@ -2894,8 +2208,8 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
     if (rc) return rc;
     CommArgs a{x, pi, mu, inv_cov, V, d, K, (float)((double)beta / (double)K), lr, iters};
     const int variant = current_opts().community_async;
-    if (variant < 1 || variant > 3)
-        return set_error(COME_E_INVALID, "community_async must be 1, 2 or 3 (got %d)", variant);
+    if (variant != 2 && variant != 3)
+        return set_error(COME_E_INVALID, "community_async must be 2 or 3 (got %d)", variant);
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 && ((uintptr_t)mu % 16) == 0 &&
         variant == 3) {
         // k_comm_split3 (the bf16 part images of every inv_cov[k], once per call) + k_community_bf3
@@ -2929,25 +2243,19 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
         return hip_error(hipGetLastError(), "k_community_bf3 launch");
     }
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 && ((uintptr_t)mu % 16) == 0) {
-        // 2 (default): k_community16; 1: the 32x32 fallback k_community_async
-        void (*kern)(CommArgs) = variant == 2 ? (d == 64 ? k_community16<64> : k_community16<128>)
-                                              : (d == 64 ? k_community_async<64>
-                                                         : k_community_async<128>);
-        const size_t lds = sizeof(float) *
-                           (size_t)(variant == 2 ? (d == 64 ? Comm16<64>::LDS_FLOATS
-                                                            : Comm16<128>::LDS_FLOATS)
-                                                 : (d == 64 ? CommAsync<64>::LDS_FLOATS
-                                                            : CommAsync<128>::LDS_FLOATS));
+        // 2: the fp32 form k_community16
+        void (*kern)(CommArgs) = d == 64 ? k_community16<64> : k_community16<128>;
+        const size_t lds =
+            sizeof(float) * (size_t)(d == 64 ? Comm16<64>::LDS_FLOATS : Comm16<128>::LDS_FLOATS);
         static bool attr = false;
         if (!attr) {
-            for (void (*f)(CommArgs) : {k_community16<64>, k_community16<128>,
-                                        k_community_async<64>, k_community_async<128>})
+            for (void (*f)(CommArgs) : {k_community16<64>, k_community16<128>})
                 (void)hipFuncSetAttribute((const void *)f,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr = true;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)((V + 127) / 128)), dim3(variant == 2 ? 512 : 256),
-                           lds, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((V + 127) / 128)), dim3(512), lds,
+                           (hipStream_t)stream, a);
         return hip_error(hipGetLastError(), "community MFMA launch");
     }
     if (d > 128) {
@@ -3095,23 +2403,7 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
                                dim3(256), lds16, (hipStream_t)stream, b);
             return hip_error(hipGetLastError(), "k_gmm_resp16_full launch");
         }
-        if (r16 != 0)
-            return set_error(COME_E_INVALID, "gmm_resp16 must be 0, 2 or 3 (got %d)", r16);
-        // 0: the 32x32x2 fallback k_gmm_resp_mfma
-        const unsigned grid = (unsigned)((V + 127) / 128);
-        const size_t lds = sizeof(float) * (size_t)(d == 64 ? RespShape<64>::LDS
-                                                             : RespShape<128>::LDS);
-        void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_mfma<64> : k_gmm_resp_mfma<128>;
-        static bool attr_m = false;
-        if (!attr_m) {
-            (void)hipFuncSetAttribute((const void *)k_gmm_resp_mfma<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_gmm_resp_mfma<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr_m = true;
-        }
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
-        return hip_error(hipGetLastError(), "k_gmm_resp_mfma launch");
+        return set_error(COME_E_INVALID, "gmm_resp16 must be 2 or 3 (got %d)", r16);
     }
     if (d > 128) {
         const size_t lds = sizeof(float) * ((size_t)2 * kTRW * d +
@@ -3173,11 +2465,10 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
-    // gmm_cov_async: 4 (default) = k_gmm_cov_bf3 (bf16 parts), 3 = k_gmm_cov16 (fp32 16x16x4),
-    // 1 = the 32x32 fp32 fallback k_gmm_cov_async
+    // gmm_cov_async: 4 (default) = k_gmm_cov_bf3 (bf16 parts), 3 = k_gmm_cov16 (fp32 16x16x4)
     const int cv = current_opts().gmm_cov_async;
-    if (cv != 1 && cv != 3 && cv != 4)
-        return set_error(COME_E_INVALID, "gmm_cov_async must be 1, 3 or 4 (got %d)", cv);
+    if (cv != 3 && cv != 4)
+        return set_error(COME_E_INVALID, "gmm_cov_async must be 3 or 4 (got %d)", cv);
     if (mfma && cv == 4) {
         static bool attr4 = false;
         if (!attr4) {
@@ -3198,15 +2489,9 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
-    void (*kern)(CovArgs) = !mfma     ? k_gmm_cov_valu
-                            : cv == 3 ? (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>)
-                                      : (d == 64 ? k_gmm_cov_async<64> : k_gmm_cov_async<128>);
-    const int threads = !mfma     ? 256
-                        : cv == 3 ? (d == 64 ? Cov16<64>::THREADS : Cov16<128>::THREADS)
-                                  : CovShape<128>::ATHREADS;
-    const int cpw = !mfma     ? 1
-                    : cv == 3 ? (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW)
-                              : (d == 64 ? CovShape<64>::CPW : CovShape<128>::CPW);
+    void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu : (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>);
+    const int threads = !mfma ? 256 : (d == 64 ? Cov16<64>::THREADS : Cov16<128>::THREADS);
+    const int cpw = !mfma ? 1 : (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW);
     hipLaunchKernelGGL(kern, dim3((K + cpw - 1) / cpw, used), dim3(threads), 0,
                        (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");

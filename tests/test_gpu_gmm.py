@@ -81,14 +81,13 @@ def test_estep_vs_numpy(V, K, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("r16", [0, 2, 3])
+@pytest.mark.parametrize("r16", [2, 3])
 def test_estep_mixed_factor_shapes(d, r16):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
     loop.  Mixed in one launch, every component must match the float64 quadratic form -- for the
-    bf16-part k_gmm_resp_bf3 (gmm_resp16 = 3) and k_gmm_resp16t (= 2) -- a lower or dense factor
-    in the launch sends every component to the separate k_gmm_resp16_full launch -- and the 32x32
-    fallback k_gmm_resp_mfma (gmm_resp16 = 0: per-component flags)."""
+    bf16-part k_gmm_resp_bf3 (gmm_resp16 = 3) and the fp32 k_gmm_resp16t (= 2): a lower or dense
+    factor in the launch sends every component to the separate k_gmm_resp16_full launch."""
     V, K = 1500, 6
     rng = np.random.RandomState(d)
     X = rng.standard_normal((V, d)).astype(np.float32)
@@ -116,10 +115,9 @@ def test_estep_mixed_factor_shapes(d, r16):
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (70_001, 7, 64), (300, 3, 64), (129, 1, 128),
                                    (1, 4, 128), (5000, 2, 128)])
 def test_estep_default_and_fallback_agree(V, K, d):
-    """The E-step forms -- k_gmm_resp_bf3 (bf16 parts), k_gmm_resp16t (16-wide fp32 blocks) and
-    the 32x32 fallback k_gmm_resp_mfma -- on sklearn-shaped upper factors, ragged row counts: the
-    same quantities summed in different orders, equal to float tolerance, responsibilities summing
-    to 1."""
+    """The E-step forms -- k_gmm_resp_bf3 (bf16 parts) and k_gmm_resp16t (16-wide fp32 blocks) --
+    on sklearn-shaped upper factors, ragged row counts: the same quantities summed in different
+    orders, equal to float tolerance, responsibilities summing to 1."""
     rng = np.random.RandomState(V + 7 * K)
     X = rng.standard_normal((V, d)).astype(np.float32)
     P = np.stack([np.triu(rng.standard_normal((d, d)) / np.sqrt(d)) + 2 * np.eye(d)
@@ -129,19 +127,18 @@ def test_estep_default_and_fallback_agree(V, K, d):
     ln = np.log(rng.dirichlet(np.ones(K)))
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev())  # noqa: E731
     out = {}
-    for r16 in (3, 2, 0):
+    for r16 in (3, 2):
         with opts(gmm_resp16=r16):
             resp, lse = gmm.estep(t(X), t(P), t(mp), t(ln))
         out[r16] = resp.cpu().numpy(), lse.cpu().numpy()
-    for r16 in (3, 2):
         assert np.isfinite(out[r16][0]).all() and np.abs(out[r16][0].sum(1) - 1).max() < 1e-4
-        np.testing.assert_allclose(out[r16][0], out[0][0], atol=1e-4)
-        np.testing.assert_allclose(out[r16][1], out[0][1], rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(out[3][0], out[2][0], atol=1e-4)
+    np.testing.assert_allclose(out[3][1], out[2][1], rtol=1e-5, atol=1e-3)
 
 
 def test_variant_options_outside_the_kept_set_are_rejected():
-    """The launch options that pick a GMM / community kernel accept only the default and its one
-    fallback (include/come.h); any other value fails the call with COME_E_INVALID instead of
+    """The launch options that pick a GMM / community kernel accept only the default (bf16 parts)
+    and its one fallback (the fp32-MFMA form; include/come.h); any other value fails the call with COME_E_INVALID instead of
     silently running some other kernel."""
     from come_amd import _lib
     from come_amd import community_embeddings as ce
@@ -152,15 +149,15 @@ def test_variant_options_outside_the_kept_set_are_rejected():
     P = t(np.stack([np.eye(d)] * K))
     mp, ln = t(np.zeros((K, d))), t(np.log(np.full(K, 1.0 / K)))
     R = t(rng.dirichlet(np.ones(K), V))
-    for bad in (1, 4, 7, 16, 19):
+    for bad in (0, 1, 4, 7, 16, 19):
         with opts(gmm_resp16=bad):
             with pytest.raises(_lib.ComeError, match="gmm_resp16"):
                 gmm.estep(X, P, mp, ln)
-    for bad in (0, 2, 5):
+    for bad in (0, 1, 2, 5):
         with opts(gmm_cov_async=bad):
             with pytest.raises(_lib.ComeError, match="gmm_cov_async"):
                 gmm.scatter(X, R, mp)
-    for bad in (0, 4):
+    for bad in (0, 1, 4):
         with opts(community_async=bad):
             with pytest.raises(_lib.ComeError, match="community_async"):
                 ce.community_grad(X.clone(), R, mp, P, 0.01, 0.1, 1)
@@ -169,7 +166,7 @@ def test_variant_options_outside_the_kept_set_are_rejected():
 @pytest.mark.parametrize("V,K,d,chunks", [(5000, 3, 64, None), (4097, 5, 128, 7),
                                           (300, 2, 128, 1), (1000, 4, 8, 3), (999, 3, 96, None),
                                           (1500, 3, 256, 4), (200, 2, 330, None)])
-@pytest.mark.parametrize("cov", [1, 3, 4])
+@pytest.mark.parametrize("cov", [3, 4])
 def test_scatter_vs_numpy(V, K, d, chunks, cov):
     rng = np.random.RandomState(V + K)
     X = rng.normal(size=(V, d)).astype(np.float32)
@@ -268,21 +265,19 @@ def test_community2vec_distributed_flag_single_process_matches():
                                           (5000, 3, 64, None), (65, 4, 64, 2), (700, 1, 128, 3),
                                           (517, 7, 64, 2), (1031, 9, 64, None)])
 def test_scatter_default_and_fallback_agree(V, K, d, chunks):
-    """k_gmm_cov16 (16x16x4 tiles), the bf16-part k_gmm_cov_bf3 (E^T E, E = sqrt(r) (x - m)) and
-    the 32x32 fallback k_gmm_cov_async (2 (d=128) / 4
-    (d=64) components per workgroup, operands centred and weighted once per block into
-    transposed LDS images, the same fp32 products): equal up to the order the MFMAs accumulate
-    the samples in (atol 1e-5 of the matrix scale), symmetric (off-diagonal tiles are stored
-    transposed; inside a diagonal tile (w x_a) x_b and (w x_b) x_a round apart, as sklearn's
-    np.dot(resp * diff.T, diff) does).  K not a multiple of the components per workgroup
-    included."""
+    """The fp32 k_gmm_cov16 (16x16x4 tiles) and the bf16-part k_gmm_cov_bf3 (E^T E, E = sqrt(r)
+    (x - m); 2 (d=128) / 4 (d=64) components per workgroup, operands centred and weighted once
+    per block into transposed LDS images): equal up to the order and form of the products (atol
+    1e-5 of the matrix scale), symmetric (off-diagonal tiles are stored transposed; inside a
+    diagonal tile (w x_a) x_b and (w x_b) x_a round apart, as sklearn's np.dot(resp * diff.T,
+    diff) does).  K not a multiple of the components per workgroup included."""
     rng = np.random.RandomState(V + K + d)
     t = lambda a: torch.as_tensor(a, device=dev())  # noqa: E731
     x = t(rng.standard_normal((V, d)).astype(np.float32))
     resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
     mu = t(rng.standard_normal((K, d)).astype(np.float32))
     out = []
-    for opt in (3, 1, 4):
+    for opt in (3, 4):
         with opts(gmm_cov_async=opt):
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
     for o in out[1:]:
@@ -318,9 +313,9 @@ def test_community2vec_trains_at_d256():
 
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (1000, 5, 128), (2049, 9, 64), (300, 3, 64),
                                    (129, 1, 128)])
-@pytest.mark.parametrize("r16", [0, 2, 3])
+@pytest.mark.parametrize("r16", [2, 3])
 def test_estep_upper_factors_vs_float64(V, K, d, r16):
-    """k_gmm_resp_bf3 (gmm_resp16 = 3), k_gmm_resp16t (= 2) and the fallback k_gmm_resp_mfma (= 0) with
+    """k_gmm_resp_bf3 (gmm_resp16 = 3) and k_gmm_resp16t (= 2) with
     sklearn-shaped (upper-triangular) precision factors only -- the launches that take the
     triangular skip -- against the float64 quadratic form, ragged rows."""
     from scipy.special import logsumexp
