@@ -6,7 +6,7 @@
   --workload c4   BASELINE configs[3]: 1M nodes, K=50, d=128: the community-gradient pass
                   (come_community_grad, iters=1) and the GMM responsibility pass
                   (come_gmm_resp); each 2*V*K*d^2 flops; roofline = fp32 MFMA peak 157.3 TFLOP/s
-                  (k_community_bf3: the bf16 MFMA peak / 6, its six bf16 part products per MAC).
+                  (k_community_b16: the bf16 MFMA peak / 6, its six bf16 part products per MAC).
   --workload walks  SURVEY.md §8f row 1, the producer of C3's input: one corpus pass over the C3
                   graph (1M-node power law, every node starts one walk, length 80) on the HIP
                   walker (come_random_walks); metric walk-steps/s; roofline: the measured 1.70
@@ -183,11 +183,11 @@ def c4(args):
     tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
     cov_kernel = {3: "k_gmm_cov16", 4: "k_gmm_cov_bf3"}[
         opts.gmm_cov_async] if ct16 else "VALU"
-    comm_kernel = {2: "k_community16", 3: "k_community_bf3"}[
+    comm_kernel = {2: "k_community16", 3: "k_community_b16"}[
         opts.community_async] if ct16 else "VALU"
-    # k_community_bf3 carries each fp32 operand as three bf16 parts and takes six part products
+    # k_community_b16 carries each fp32 operand as three bf16 parts and takes six part products
     # per multiply-add: its ceiling is the bf16 MFMA peak / 6, not the fp32 MFMA peak
-    comm_bf3 = comm_kernel == "k_community_bf3"
+    comm_bf3 = comm_kernel == "k_community_b16"
     comm_peak = BF16_MFMA_PEAK_TFLOPS / 6 if comm_bf3 else F32_MFMA_PEAK_TFLOPS
     resp_kernel = {2: "k_gmm_resp16t", 3: "k_gmm_resp_bf3"}[
         opts.gmm_resp16] if ct16 else "VALU"

@@ -271,9 +271,9 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       d <= 128, n <= 5 -- compiled for 8 waves per SIMD there -- else 6)
  *   resident_cap        1 = also clamp grids to the workgroups the occupancy API reports resident
  *   community_async     community gradient at d = 64, 128 (16-B aligned mu / inv_cov; else the
- *                       VALU kernel): default 3 = k_community_bf3 (each fp32 operand as three
- *                       bf16 parts, six exact part products per multiply-add on 32x32x16 bf16
- *                       MFMAs -- fp32-level error, tests/test_gpu_c4.py; 7.3 vs 11.5 ms at C4);
+ *                       VALU kernel): default 3 = k_community_b16 (each fp32 operand as three
+ *                       bf16 parts, six exact part products per multiply-add on 16x16x32 bf16
+ *                       MFMAs -- fp32-level error, tests/test_gpu_c4.py; 6.75 vs 11.5 ms at C4);
  *                       2 = k_community16 (fp32 16x16x4 MFMAs, one 16-row tile per wavefront;
  *                       11.5 ms).  Other values: COME_E_INVALID
  *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 4 = k_gmm_cov_bf3 (E^T E with

@@ -72,7 +72,7 @@ struct CommArgs {
     float coef;  // (float)(beta / K), community_embeddings.py:77 (numpy weak-scalar cast)
     float lr;
     int iters;
-    const void *img;  // k_community_bf3: inv_cov as k_comm_split3's bf16 part images
+    const void *img;  // k_community_b16: inv_cov as k_comm_split16's bf16 part images
 };
 
 __global__ void __launch_bounds__(kThreads) k_community_grad(CommArgs a) {
@@ -347,49 +347,15 @@ __global__ void __launch_bounds__(512, 4) k_community16(CommArgs a) {
     }
 }
 
-// ---- community gradient, fp32 operands as bf16 parts on 32x32x16 MFMAs (community_async = 3) --
+// ---- fp32 operands as bf16 parts: the arithmetic of the C4 default kernels --------------------
 //
 // Every fp32 operand v is carried as three bf16 parts, v1 = bf16(v), v2 = bf16(v - v1), v3 =
 // bf16(v - v1 - v2): each difference is exact in fp32 and |v - v1 - v2 - v3| <= 2^-27 |v|.  A
 // product a b is taken as its six part products of order <= 2 (a3 b1 + a2 b2 + a1 b3 + a2 b1 +
 // a1 b2 + a1 b1; the three dropped are below 2^-26 |a b|), each exact in fp32, summed by the MFMA
 // in fp32: the result carries fp32-level error (tests hold it to the fp32 kernels' tolerances),
-// not a reduced-precision one.  Six v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) do the work of eight
-// v_mfma_f32_32x32x2f32 (8 x 64): 2.67x the fp32 MFMA rate.
-//
-// Shape: 4 wavefronts x 32 rows per workgroup, two workgroups per CU (~190 VGPRs: 2 waves per
-// SIMD).  MFMA (column tile ct, k-step s of 16 features): A[i][k] = M_k[feat(32 ct + i)][16 s + k]
-// (one ds_read_b128 per part from the image k_comm_split3 wrote), B[k][j] = pi_jk (x_j -
-// mu_k)[16 s + k] split in registers (lane: row j = lane % 32, features 16 s + 8 (lane / 32) ..
-// + 7 of every step).  feat() orders the image rows so that accumulator register r of tile ct
-// belongs to the lane's own x[2 ct + r / 8][r % 8]: the update happens in registers.  M_k's image
-// is staged in quarters (2 k-steps, 24 KB at d = 128), two quarter buffers, one barrier per
-// quarter; quarter t + 2 is copied by LDS-DMA while t + 1 is multiplied.  (Measured and not
-// kept, profiles/r06_ab_community_bf3.txt: explicit MFMA / VALU sched groups; a sched_barrier-
-// pinned pipeline reading the next block's A parts into the registers each block frees and
-// splitting one B pair per block: 7.24 vs 7.16 ms; 8-wavefront workgroups, half-component units.)
-template <int D>
-struct CommBf3 {
-    static constexpr int NS = D / 16;           // k-steps of 16 features
-    static constexpr int NQ = D / 32;           // quarters (2 k-steps each)
-    static constexpr int CT = D / 32;           // 32-wide output column tiles
-    static constexpr int PLANE = 2 * D * 32;    // bytes per part within a quarter (2 steps x D rows x 32 B)
-    static constexpr int QBYTES = 3 * PLANE;    // 24 KB at d = 128
-    // output feature of image row rho: the 32x32x16 accumulator holds row i = (r & 3) + 8 (r >> 2)
-    // + 4 h of a tile in register r on lane half h; this order sends it to feature 16 (2 ct + r / 8)
-    // + 8 h + r % 8, the one x[2 ct + r / 8][r % 8] of the lane holds
-    __host__ __device__ static constexpr int feat(int rho) {
-        const int ct = rho >> 5, i = rho & 31;
-        return 16 * (2 * ct + (i >> 4)) + 8 * ((i >> 2) & 1) + 4 * ((i >> 3) & 1) + (i & 3);
-    }
-    // byte offset in a quarter of (part P, step sl, row rho, 16-B granule g): two granules per
-    // row, swapped on rows with bit 4 set (the lane groups of ds_read_b128 then hit 16 distinct
-    // 4-bank groups)
-    __host__ __device__ static constexpr int at(int P, int sl, int rho, int g) {
-        return P * PLANE + (sl * D + rho) * 32 + 16 * (g ^ ((rho >> 4) & 1));
-    }
-};
-
+// not a reduced-precision one.  A 16x16x32 block costs six v_mfma_f32_16x16x32_bf16 (6 x 16
+// cycles) instead of eight v_mfma_f32_16x16x4_f32 (8 x 32): 2.67x the fp32 MFMA rate.
 // bf16 part arithmetic on packed pairs (element 0 in the low half)
 __device__ __forceinline__ uint32_t bf16_pk(float lo, float hi) {
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -411,113 +377,110 @@ __device__ __forceinline__ void bf16_split3(float lo, float hi, uint32_t &p1, ui
     p3 = bf16_pk(l2 - bf16_lo(p2), h2 - bf16_hi(p2));
 }
 
-// inv_cov [K][D][D] -> per component and quarter the LDS image of CommBf3 (thread: one row,
-// step and granule = 8 consecutive features, its three parts)
+// ---- community gradient on bf16 parts, 16x16x32 MFMAs (k_community_b16, community_async = 3) ---
+//
+// One 16-row tile per wavefront, 8 wavefronts per 128-row workgroup: the fp32 kernel's wave shape
+// (128 VGPRs: 4 waves per SIMD) on v_mfma_f32_16x16x32_bf16 (16 cycles).  M_k is split once per
+// call (k_comm_split16); the row side pi_ik (x_i - mu_k) is split in registers at each step's head
+// (the other three waves of the SIMD cover that VALU).  6.75 ms at C4 against 7.54 for the round-5
+// first form (32x32x16 tiles, 32 rows per wavefront, ~216 VGPRs: 2 waves per SIMD, the next step's
+// split software-pipelined), profiles/r06_ab_community_bf3.txt.  Lane (row j = lane % 16, group
+// kg = lane / 16) holds features 32 s + 8 kg .. + 7 of its row for each 32-feature step s; image
+// row 16 ct + i of M_k is output feature feat(), so accumulator register r of tile ct (row
+// 4 kg + r) is the lane's own x[ct / 2][ct % 2][r].  One step (3 parts x D rows x 64 B, 24 KB at
+// d = 128) is one staging unit, two buffers, one barrier per unit.
 template <int D>
-__global__ void __launch_bounds__(256) k_comm_split3(const float *__restrict__ M,
-                                                     char *__restrict__ img, int K) {
-    using C = CommBf3<D>;
-    const int64_t n = (int64_t)K * C::NQ * 2 * D * 2;
+struct CommB16 {
+    static constexpr int NS = D / 32;            // k-steps of 32 features = staging units
+    static constexpr int CT = D / 16;            // 16-wide output column tiles
+    static constexpr int PART = D * 64;          // bytes per part of a step
+    static constexpr int UBYTES = 3 * PART;
+    static constexpr int NW = 8;
+    static constexpr int MUS = 2 * UBYTES;       // mu[2][256] after the two unit buffers
+    static constexpr int LDS_BYTES = MUS + 2 * 1024;
+    static constexpr int PIECES = UBYTES / 1024;
+    __host__ __device__ static constexpr int feat(int rho) {
+        const int ct = rho >> 4, i = rho & 15;
+        return 32 * (ct >> 1) + 8 * (i >> 2) + 4 * (ct & 1) + (i & 3);
+    }
+    // (part P, image row rho, 16-B granule g of the step): granules swizzled by bit 2 of the row
+    // (exhaustive search: conflict-free for the four 16-lane ds_read_b128 groups)
+    __host__ __device__ static constexpr int at(int P, int rho, int g) {
+        return P * PART + rho * 64 + 16 * (g ^ (((rho >> 2) & 1) << 1));
+    }
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) k_comm_split16(const float *__restrict__ M,
+                                                      char *__restrict__ img, int K) {
+    using C = CommB16<D>;
+    const int64_t n = (int64_t)K * C::NS * D * 4;
     for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n;
          t += (int64_t)gridDim.x * 256) {
-        const int g = (int)(t & 1);
-        const int rho = (int)((t >> 1) % D);
-        const int sl = (int)((t >> 1) / D % 2);
-        const int64_t kq = (t >> 1) / D / 2;  // k * NQ + q
-        const int q = (int)(kq % C::NQ);
-        const int64_t k = kq / C::NQ;
-        const float *src = M + (k * D + C::feat(rho)) * D + 16 * (2 * q + sl) + 8 * g;
+        const int g = (int)(t & 3);
+        const int rho = (int)((t >> 2) % D);
+        const int64_t ks = (t >> 2) / D;  // k * NS + s
+        const int st = (int)(ks % C::NS);
+        const int64_t k = ks / C::NS;
+        const float *src = M + (k * D + C::feat(rho)) * D + 32 * st + 8 * g;
         uint4 w[3];
         uint32_t *w1 = &w[0].x, *w2 = &w[1].x, *w3 = &w[2].x;
 #pragma unroll
         for (int e = 0; e < 4; ++e) bf16_split3(src[2 * e], src[2 * e + 1], w1[e], w2[e], w3[e]);
-        char *qb = img + kq * C::QBYTES;
+        char *ub = img + ks * C::UBYTES;
 #pragma unroll
-        for (int P = 0; P < 3; ++P) *reinterpret_cast<uint4 *>(qb + C::at(P, sl, rho, g)) = w[P];
+        for (int P = 0; P < 3; ++P) *reinterpret_cast<uint4 *>(ub + C::at(P, rho, g)) = w[P];
     }
 }
 
-// quarter t of the images -> LDS buffer b (QBYTES / 1 KiB LDS-DMA pieces over 4 wavefronts)
-// Launch shape of k_community_bf3: NW wavefronts (32 rows each) per workgroup, M_k staged in
-// units of SG k-steps (SG / 2 quarters), two unit buffers, one barrier per unit.
-template <int D, int NW, int SG>
-struct CommBf3Shape {
-    static constexpr int NU = D / 16 / SG;                        // units per component
-    static constexpr int UBYTES = SG / 2 * CommBf3<D>::QBYTES;
-    static constexpr int MUS = 2 * UBYTES;                        // mu[2][256] after the buffers
-    static constexpr int LDS_BYTES = MUS + 2 * 1024;
-    static constexpr int PIECES = UBYTES / 1024;
-    static_assert(NU >= 2 && NU % 2 == 0 && PIECES % 4 == 0, "unit shape");
-};
-#ifndef COME_BF3_SHAPE
-#define COME_BF3_SHAPE 0
-#endif
-// the product shape per d: (NW, SG) = (4, 2) -- two 4-wavefront workgroups per CU, quarter units
 template <int D>
-struct CommBf3Pick {
-    static constexpr int NW = COME_BF3_SHAPE == 0 ? 4 : 8;
-    static constexpr int SG = (COME_BF3_SHAPE == 1 && D == 128) ? 4 : 2;
-    using S = CommBf3Shape<D, NW, SG>;
-};
-
-// unit t of the images -> LDS buffer b (1 KiB LDS-DMA pieces over the NW wavefronts)
-template <int D, int NW, int SG>
-__device__ __forceinline__ void commbf3_stage(const char *gimg, int64_t t, char *smb, int b,
-                                              int wid, int lane) {
-    using S = CommBf3Shape<D, NW, SG>;
-    const char *src = gimg + t * S::UBYTES + 16 * lane;
-#pragma unroll
-    for (int j = 0; j < (S::PIECES + NW - 1) / NW; ++j) {
-        const int i = wid + NW * j;
-        if (S::PIECES % NW != 0 && i >= S::PIECES) break;  // wavefront-uniform
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const float *>(src + i * 1024),
-                                         reinterpret_cast<float *>(smb + b * S::UBYTES + i * 1024),
-                                         16, 0, 0);
-    }
-}
-
-template <int D, int NW, int SG>
-__device__ __forceinline__ void commbf3_stage_mu(const float *mu, char *smb, int buf, int wid,
-                                                 int lane) {
-    if (wid == 0) {
-        const int src = lane * 4 < D ? lane * 4 : D - 4;
-        __builtin_amdgcn_global_load_lds(
-            mu + src, reinterpret_cast<float *>(smb + CommBf3Shape<D, NW, SG>::MUS + buf * 1024),
-            16, 0, 0);
-    }
-}
-
-template <int D, int NW, int SG>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
-    k_community_bf3(CommArgs a) {
-    using C = CommBf3<D>;
-    using S = CommBf3Shape<D, NW, SG>;
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+    k_community_b16(CommArgs a) {
+    using C = CommB16<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
     extern __shared__ __attribute__((aligned(16))) char smb[];
     const char *gimg = reinterpret_cast<const char *>(a.img);
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int j = lane & 31, h = lane >> 5;
-    const int64_t row = (int64_t)blockIdx.x * (32 * NW) + wid * 32 + j;
+    const int j = lane & 15, kg = lane >> 4;
+    const int64_t row = (int64_t)blockIdx.x * 128 + wid * 16 + j;
     const bool rowok = row < a.V;
     const int64_t prow = rowok ? row : a.V - 1;
-    f32x4 xv[C::NS][2];  // features 16 s + 8 h + 4 u + 0..3
+    f32x4 xv[C::NS][2];  // features 32 s + 8 kg + 4 u + 0..3
 #pragma unroll
     for (int s = 0; s < C::NS; ++s)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-            xv[s][u] = rowok ? *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * s + 8 * h + 4 * u)
+            xv[s][u] = rowok ? *reinterpret_cast<const f32x4 *>(a.x + row * D + 32 * s + 8 * kg + 4 * u)
                              : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const int aoff = C::at(0, 0, j, h);  // + C::at(P, sl, 32 ct, 0) (bit 4 of 32 ct + j is j's)
-    const int nt = a.K * S::NU;
-    // B parts of step s for component mu / weight p (features 16 s + 8 h .. + 7 of the lane's row)
+    auto stage = [&](int64_t t, int b) {
+        const char *src = gimg + t * C::UBYTES + 16 * lane;
+#pragma unroll
+        for (int q = 0; q < (C::PIECES + C::NW - 1) / C::NW; ++q) {
+            const int i = wid + C::NW * q;
+            if (C::PIECES % C::NW != 0 && i >= C::PIECES) break;  // wavefront-uniform
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const float *>(src + i * 1024),
+                                             reinterpret_cast<float *>(smb + b * C::UBYTES + i * 1024),
+                                             16, 0, 0);
+        }
+    };
+    auto stage_mu = [&](int c, int b) {
+        if (wid == 0) {
+            const int src = lane * 4 < D ? lane * 4 : D - 4;
+            __builtin_amdgcn_global_load_lds(a.mu + (int64_t)c * D + src,
+                                             reinterpret_cast<float *>(smb + C::MUS + b * 1024), 16,
+                                             0, 0);
+        }
+    };
+    auto mus_of = [&](int k) {
+        return reinterpret_cast<const float *>(smb + C::MUS + (k & 1) * 1024);
+    };
     auto split = [&](int s, const float *mus, float p, bf16x8 (&B)[3]) {
         uint32_t bw[3][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const f32x4 m = *reinterpret_cast<const f32x4 *>(mus + 16 * s + 8 * h + 4 * u);
+            const f32x4 m = *reinterpret_cast<const f32x4 *>(mus + 32 * s + 8 * kg + 4 * u);
             float b[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) b[e] = p * (xv[s][u][e] - m[e]);
@@ -528,86 +491,61 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
         for (int P = 0; P < 3; ++P)
             B[P] = __builtin_bit_cast(bf16x8, uint4{bw[P][0], bw[P][1], bw[P][2], bw[P][3]});
     };
-    auto mus_of = [&](int k) {
-        return reinterpret_cast<const float *>(smb + S::MUS + (k & 1) * 1024);
-    };
+    const int aoff = C::at(0, j, kg);  // + C::at(0, 16 ct, 0): bit 2 of 16 ct + j is j's
+    const int nt = a.K * C::NS;
     for (int it = 0; it < a.iters; ++it) {
         __syncthreads();  // the previous iteration's buffers are free
-        commbf3_stage<D, NW, SG>(gimg, 0, smb, 0, wid, lane);
-        commbf3_stage<D, NW, SG>(gimg, 1, smb, 1, wid, lane);
-        commbf3_stage_mu<D, NW, SG>(a.mu, smb, 0, wid, lane);
-        commbf3_stage_mu<D, NW, SG>(a.mu + (int64_t)min(1, a.K - 1) * D, smb, 1, wid, lane);
-        // pi loads unconditional (row clamped, zeroed when used): a load under a divergent
-        // branch makes the compiler drain every load in flight before the next use
+        stage(0, 0);
+        stage(1, 1);
+        stage_mu(0, 0);
         const float p0 = a.pi[prow * a.K];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        f32x16 acc[C::CT];
+        f32x4 acc[C::CT];
 #pragma unroll
-        for (int ct = 0; ct < C::CT; ++ct)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[ct][e] = 0.0f;
-        // software pipeline: step s + 1's B parts are formed on the VALU while step s's MFMAs
-        // run (the last step of component k forms step 0 of k + 1: mu_{k+1} is staged two units
-        // ahead, pi[row, k + 1] loaded at the start of k)
-        float pc = rowok ? p0 : 0.0f;
-        bf16x8 Bc[3];
-        split(0, mus_of(0), pc, Bc);
+        for (int ct = 0; ct < C::CT; ++ct) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        float pn = p0;
         for (int k = 0; k < a.K; ++k) {
-          const float pv = a.pi[prow * a.K + min(k + 1, a.K - 1)];
+          const float pc = rowok ? pn : 0.0f;
+          pn = a.pi[prow * a.K + min(k + 1, a.K - 1)];
 #pragma unroll
-          for (int u = 0; u < S::NU; ++u) {
-            const int t = k * S::NU + u;
-            const char *ub = smb + (u & 1) * S::UBYTES;  // t & 1 (NU is even)
+          for (int s = 0; s < C::NS; ++s) {
+            const int t = k * C::NS + s;
+            const char *ub = smb + (s & 1) * C::UBYTES;  // t & 1 (NS is even)
+            // B parts at the step's head (4 waves per SIMD cover the VALU; no second register set)
+            bf16x8 Bc[3];
+            split(s, mus_of(k), pc, Bc);
 #pragma unroll
-            for (int si = 0; si < SG; ++si) {
-                const int s = SG * u + si;
-                bf16x8 Bn[3];
-                if (s + 1 < C::NS) split(s + 1, mus_of(k), pc, Bn);
-                else split(0, mus_of(k + 1), rowok ? pv : 0.0f, Bn);  // (unused after the last k)
+            for (int ct = 0; ct < C::CT; ++ct) {
+                const char *base = ub + C::at(0, 16 * ct, 0) + aoff;
+                bf16x8 A[3];
 #pragma unroll
-                for (int ct = 0; ct < C::CT; ++ct) {
-                    const char *base = ub + (si / 2) * C::QBYTES + C::at(0, si % 2, 32 * ct, 0) + aoff;
-                    bf16x8 A[3];
-#pragma unroll
-                    for (int P = 0; P < 3; ++P)
-                        A[P] = *reinterpret_cast<const bf16x8 *>(base + P * C::PLANE);
-                    // small parts first
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], Bc[0], acc[ct], 0, 0, 0);
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], Bc[1], acc[ct], 0, 0, 0);
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], Bc[2], acc[ct], 0, 0, 0);
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], Bc[0], acc[ct], 0, 0, 0);
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], Bc[1], acc[ct], 0, 0, 0);
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], Bc[0], acc[ct], 0, 0, 0);
-                }
-#pragma unroll
-                for (int P = 0; P < 3; ++P) Bc[P] = Bn[P];
+                for (int P = 0; P < 3; ++P) A[P] = *reinterpret_cast<const bf16x8 *>(base + P * C::PART);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], Bc[0], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], Bc[1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], Bc[2], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], Bc[0], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], Bc[1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], Bc[0], acc[ct], 0, 0, 0);
             }
             if (t + 1 < nt) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();  // buffer t & 1 free; unit t + 1 in LDS
-                if (t + 2 < nt) commbf3_stage<D, NW, SG>(gimg, t + 2, smb, u & 1, wid, lane);
-                // mu_c, c = (t + 3) / NU, into buffer c & 1 (last read by component c - 2's
-                // steps, all before this barrier); it lands by the barrier after unit t + 1,
-                // before the last step of component c - 1 reads it
-                if ((u + 3) % S::NU == 0) {
-                    const int c = k + (u + 3) / S::NU;
-                    if (c >= 2 && c < a.K)
-                        commbf3_stage_mu<D, NW, SG>(a.mu + (int64_t)c * D, smb, c & 1, wid, lane);
-                }
+                if (t + 2 < nt) stage(t + 2, s & 1);
+                // mu_{k+1} into buffer (k + 1) & 1 (component k - 1's, done) with the unit that
+                // opens component k + 1; it lands by that unit's barrier
+                if (s + 2 == C::NS && k + 1 < a.K) stage_mu(k + 1, (k + 1) & 1);
             }
           }
-          pc = rowok ? pv : 0.0f;
         }
-        // x -= lr * clip(coef * G, -5, 5): register r of tile ct is x[2 ct + r / 8][r % 8]
+        // x -= lr * clip(coef * G, -5, 5): register r of tile ct is x[ct / 2][ct % 2][r]
 #pragma unroll
         for (int ct = 0; ct < C::CT; ++ct)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int r = 0; r < 4; ++r) {
                 float g = acc[ct][r] * a.coef;
                 g = g < -5.0f ? -5.0f : (g > 5.0f ? 5.0f : g);
-                const int e = r & 7;
-                xv[2 * ct + (r >> 3)][e >> 2][e & 3] -= g * a.lr;
+                xv[ct >> 1][ct & 1][r] -= g * a.lr;
             }
     }
     if (rowok) {
@@ -615,7 +553,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
         for (int s = 0; s < C::NS; ++s)
 #pragma unroll
             for (int u = 0; u < 2; ++u)
-                *reinterpret_cast<f32x4 *>(a.x + row * D + 16 * s + 8 * h + 4 * u) = xv[s][u];
+                *reinterpret_cast<f32x4 *>(a.x + row * D + 32 * s + 8 * kg + 4 * u) = xv[s][u];
     }
 }
 
@@ -1142,10 +1080,10 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
 
 // ---- E-step on bf16-part MFMAs (k_gmm_resp_bf3, gmm_resp16 = 3) -----------------------------
 //
-// k_community_bf3's arithmetic (fp32 operands as three bf16 parts, six exact part products per
+// The bf16-part arithmetic (fp32 operands as three bf16 parts, six exact part products per
 // multiply-add, summed in fp32) on Y = X P_k: output D[i][j] = Y[row j][32 ct + i] of column
 // tile ct, A = P_k^T parts (LDS), B = the row's x parts -- x does not change over the components,
-// so the row side is split ONCE per workgroup, not per component (k_community_bf3's VALU cost).
+// so the row side is split ONCE per workgroup, not per component (the community step's VALU cost).
 // Upper factors only (sklearn's precisions_cholesky_): tile ct needs k-steps s <= 2 ct + 1, 20 of
 // the 32 (ct, s) blocks at d = 128 (6 of 8 at d = 64); a launch holding a lower or dense factor
 // returns at once and k_gmm_resp16_full runs it.  Each block's three parts are one 3 KiB image
@@ -1167,7 +1105,9 @@ struct RespBf3 {
                 ++n;
             }
     }
-    // byte offset in a block image of (part P, row i, 16-B granule g), swizzled as CommBf3::at
+    // byte offset in a block image of (part P, row i, 16-B granule g): two granules per 32-B row,
+    // swapped on rows with bit 4 set (the lane groups of ds_read_b128 then hit 16 distinct 4-bank
+    // groups)
     __host__ __device__ static constexpr int at(int P, int i, int g) {
         return P * 1024 + i * 32 + 16 * (g ^ ((i >> 4) & 1));
     }
@@ -1779,7 +1719,7 @@ __global__ void __launch_bounds__((Cov16<D>::THREADS))
 //
 // S_k = sum_i r_ik d_i d_i^T (d_i = x_i - m_k) written as E^T E with E_ik = sqrt(r_ik) d_i: one
 // operand image serves both sides of every MFMA.  E is formed and split into its three bf16 parts
-// (k_community_bf3's arithmetic: six exact part products per multiply-add, summed in fp32) by 4
+// (the bf16-part arithmetic: six exact part products per multiply-add, summed in fp32) by 4
 // staging wavefronts, ONCE per (sample, feature, component), into a feature-major LDS image (rows
 // of 32 samples, 16-byte granules of 8 samples XOR-swizzled by CovBf3::swz: conflict-free
 // ds_read_b128 fragments and ds_write_b128 stores).  The MFMA wavefronts take fragment a (32
@@ -2212,35 +2152,29 @@ extern "C" int come_community_grad(float *x, int64_t V, int d, const float *pi, 
         return set_error(COME_E_INVALID, "community_async must be 2 or 3 (got %d)", variant);
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 && ((uintptr_t)mu % 16) == 0 &&
         variant == 3) {
-        // k_comm_split3 (the bf16 part images of every inv_cov[k], once per call) + k_community_bf3
-        const size_t qbytes = d == 64 ? CommBf3<64>::QBYTES : CommBf3<128>::QBYTES;
-        const size_t img_bytes = (size_t)K * (d / 32) * qbytes;
-        char *img = (char *)stream_scratch(dev, stream, kScratchCommSplit, img_bytes);
+        // k_comm_split16 (the bf16 part images of every inv_cov[k], once per call) + k_community_b16
+        const size_t ub = d == 64 ? CommB16<64>::UBYTES : CommB16<128>::UBYTES;
+        char *img = (char *)stream_scratch(dev, stream, kScratchCommSplit, (size_t)K * (d / 32) * ub);
         if (!img) return scratch_failed();
-        const int64_t work = (int64_t)K * (d / 32) * 2 * d * 2;
-        const unsigned sg = (unsigned)std::min<int64_t>((work + 255) / 256, 4096);
-        hipLaunchKernelGGL(d == 64 ? k_comm_split3<64> : k_comm_split3<128>, dim3(sg), dim3(256), 0,
+        const int64_t work = (int64_t)K * (d / 32) * d * 4;
+        hipLaunchKernelGGL(d == 64 ? k_comm_split16<64> : k_comm_split16<128>,
+                           dim3((unsigned)std::min<int64_t>((work + 255) / 256, 4096)), dim3(256), 0,
                            (hipStream_t)stream, inv_cov, img, K);
-        rc = hip_error(hipGetLastError(), "k_comm_split3 launch");
+        rc = hip_error(hipGetLastError(), "k_comm_split16 launch");
         if (rc) return rc;
         a.img = img;
-        using P64 = CommBf3Pick<64>;
-        using P128 = CommBf3Pick<128>;
-        void (*kern)(CommArgs) = d == 64 ? k_community_bf3<64, P64::NW, P64::SG>
-                                         : k_community_bf3<128, P128::NW, P128::SG>;
         static bool attr3 = false;
         if (!attr3) {
-            for (void (*f)(CommArgs) : {k_community_bf3<64, P64::NW, P64::SG>,
-                                        k_community_bf3<128, P128::NW, P128::SG>})
+            for (void (*f)(CommArgs) : {k_community_b16<64>, k_community_b16<128>})
                 (void)hipFuncSetAttribute((const void *)f,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr3 = true;
         }
-        const int nw = d == 64 ? P64::NW : P128::NW;
-        const size_t lds = d == 64 ? P64::S::LDS_BYTES : P128::S::LDS_BYTES;
-        hipLaunchKernelGGL(kern, dim3((unsigned)((V + 32 * nw - 1) / (32 * nw))), dim3(64 * nw), lds,
+        hipLaunchKernelGGL(d == 64 ? k_community_b16<64> : k_community_b16<128>,
+                           dim3((unsigned)((V + 127) / 128)), dim3(512),
+                           d == 64 ? CommB16<64>::LDS_BYTES : CommB16<128>::LDS_BYTES,
                            (hipStream_t)stream, a);
-        return hip_error(hipGetLastError(), "k_community_bf3 launch");
+        return hip_error(hipGetLastError(), "k_community_b16 launch");
     }
     if ((d == 64 || d == 128) && ((uintptr_t)inv_cov % 16) == 0 && ((uintptr_t)mu % 16) == 0) {
         // 2: the fp32 form k_community16

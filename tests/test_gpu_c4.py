@@ -81,7 +81,7 @@ def test_c4_community_grad_k50_1m(c4_rows, iters, kern):
 
 
 def test_c4_community_bf3_error_is_fp32_level(c4_rows):
-    """k_community_bf3 carries each fp32 operand as three bf16 parts and sums six exact part
+    """k_community_b16 carries each fp32 operand as three bf16 parts and sums six exact part
     products per multiply-add (|dropped terms| < 2^-26 |a b|): a product more accurate than one
     fp32 rounding, so its error against float64 must be that of the fp32-MFMA kernel
     (k_community16), not a reduced-precision one.  Unclipped update (beta/K = 0.5, lr = 1) on

@@ -378,8 +378,8 @@ _VALU_COMM = [(96, 200, 3, 2), (256, 150, 3, 2), (500, 37, 2, 1)]
                          [c + (2,) for c in _VALU_COMM])
 def test_community_grad_vs_oracle(d, V, K, iters, kern):
     """MFMA path (d = 64, 128; ragged row tiles; community_async = 2: k_community16 on fp32
-    16x16x4 MFMAs with one row tile per wavefront, 3: k_community_bf3, fp32 operands as three
-    bf16 parts on 32x32x16 MFMAs), VALU path
+    16x16x4 MFMAs with one row tile per wavefront, 3: k_community_b16, fp32 operands as three
+    bf16 parts on 16x16x32 MFMAs), VALU path
     (d = 96) and the wide VALU path (d = 256, 500: matrices streamed in row chunks) against the
     numpy restatement of community_embeddings.py:61-78: fp32 contractions in another order,
     rtol/atol 2e-5; the clip at +-5 is exercised (beta large)."""
