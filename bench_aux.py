@@ -169,7 +169,7 @@ def c4(args):
                                     orc.precision_cholesky(cov), dev)
     flops = 2.0 * V * K * d * d
     # fraction of the MFMA blocks executed on sklearn's upper-triangular precision factors: the
-    # bf16-part E-step's 32-wide column tiles x 16-feature steps (k_gmm_resp_bf3, 20 of 32 at
+    # bf16-part E-step's 16-wide column tiles x 32-feature steps (k_gmm_resp_b16, 20 of 32 at
     # d = 128) or the fp32 form's 16-wide blocks (k_gmm_resp16t, 36 of 64); the scatter's
     # symmetric 32-wide (10 of 16, k_gmm_cov_bf3) / 16-wide (36 of 64, k_gmm_cov16) tiles
     from come_amd import _lib
@@ -189,7 +189,7 @@ def c4(args):
     # per multiply-add: its ceiling is the bf16 MFMA peak / 6, not the fp32 MFMA peak
     comm_bf3 = comm_kernel == "k_community_b16"
     comm_peak = BF16_MFMA_PEAK_TFLOPS / 6 if comm_bf3 else F32_MFMA_PEAK_TFLOPS
-    resp_kernel = {2: "k_gmm_resp16t", 3: "k_gmm_resp_bf3"}[
+    resp_kernel = {2: "k_gmm_resp16t", 3: "k_gmm_resp_b16"}[
         opts.gmm_resp16] if ct16 else "VALU"
     x0 = x.clone()
     xs, pis, x0s = x[lo:hi], pi[lo:hi], x0[lo:hi]

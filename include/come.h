@@ -285,10 +285,10 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)
  *   o2_atomic_writeback direct kernel: every row update written as a float-atomic delta
- *   gmm_resp16          GMM E-step at d = 64, 128: default 3 = k_gmm_resp_bf3 (fp32 operands
- *                       as three bf16 parts, six exact part products per multiply-add on 32x32x16
- *                       bf16 MFMAs, the row's parts formed once; 32-wide triangular skip; 4.5 ms
- *                       at C4); 2 = k_gmm_resp16t on fp32 16x16x4 MFMAs (16-wide triangular skip,
+ *   gmm_resp16          GMM E-step at d = 64, 128: default 3 = k_gmm_resp_b16 (fp32 operands
+ *                       as three bf16 parts, six exact part products per multiply-add on 16x16x32
+ *                       bf16 MFMAs, the row's parts formed once, 4 waves per SIMD; 4.1 ms at
+ *                       C4); 2 = k_gmm_resp16t on fp32 16x16x4 MFMAs (16-wide triangular skip,
  *                       in-lane row sums, the factors' non-zero 16x16 blocks packed, whole
  *                       components double-buffered, one barrier per component; 6.95 ms); a
  *                       launch holding a lower or dense factor runs every block, in

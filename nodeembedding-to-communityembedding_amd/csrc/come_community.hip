@@ -1078,89 +1078,62 @@ __global__ void __launch_bounds__(R16tShape::THREADS, R16tShape::WPE) k_gmm_resp
     }
 }
 
-// ---- E-step on bf16-part MFMAs (k_gmm_resp_bf3, gmm_resp16 = 3) -----------------------------
+// ---- E-step on bf16 parts, 16x16x32 MFMAs (k_gmm_resp_b16, gmm_resp16 = 3) -------------------
 //
 // The bf16-part arithmetic (fp32 operands as three bf16 parts, six exact part products per
-// multiply-add, summed in fp32) on Y = X P_k: output D[i][j] = Y[row j][32 ct + i] of column
-// tile ct, A = P_k^T parts (LDS), B = the row's x parts -- x does not change over the components,
-// so the row side is split ONCE per workgroup, not per component (the community step's VALU cost).
-// Upper factors only (sklearn's precisions_cholesky_): tile ct needs k-steps s <= 2 ct + 1, 20 of
-// the 32 (ct, s) blocks at d = 128 (6 of 8 at d = 64); a launch holding a lower or dense factor
-// returns at once and k_gmm_resp16_full runs it.  Each block's three parts are one 3 KiB image
-// (k_pack_upper_bf3); a component is staged in NU units of NB / NU blocks, two unit buffers, one
-// barrier per unit, mu_k P_k and log_norm_k beside it.  A row's sum of squares: 64 in-lane FMAs
-// and one permlane32 swap (the 32x32 accumulator holds 16 columns of one row per lane half).
+// multiply-add, summed in fp32) on Y = X P_k: output D[i][j] = Y[row j][16 ct + i], A = P_k^T parts
+// (LDS), B = the row's x parts -- x does not change over the components, so the row side is split
+// ONCE per workgroup, not per component (the community step's VALU cost).  Upper factors only
+// (sklearn's precisions_cholesky_); a launch holding a lower or dense factor returns at once and
+// k_gmm_resp16_full runs it.  k_community_b16's wave shape: one 16-row tile per wavefront, 8
+// wavefronts per 128-row workgroup, the row's parts (48 VGPRs) formed once, 128 VGPRs: 4 waves
+// per SIMD.  A component is staged in two units of 10 blocks, mu_k P_k and log_norm_k beside the
+// first; each tile's first MFMA starts from the constant 0 and its squared residuals are summed as
+// soon as its last block completes.  4.12 ms at C4 against 4.54 for the round-5 first form
+// (32x32x16 tiles, 32 rows per wavefront, 2 waves per SIMD, A parts read one block ahead; removed),
+// profiles/r06_ab_estep_bf3.txt.
+// Block (16-wide column tile ct, 32-feature step s) of P_k^T is non-zero iff s <= ct / 2: 20 of 32
+// at d = 128 (6 of 8 at 64), each a 3 KiB image (3 parts x 16 rows x 64 B, granules swizzled by
+// bit 2 of the row as CommB16::at).  Lane (row j, group kg) holds columns 16 ct + 4 kg .. + 3 of
+// its row per tile: a row's sum of squares is 4 x (tiles) in-lane FMAs and two permlane swaps.
 template <int D>
-struct RespBf3 {
-    static constexpr int NS = D / 16, CT = D / 32;
-    static constexpr int NB = CT * (CT + 1);  // sum over ct of 2 ct + 2
-    static constexpr int BLK = 3 * 1024;      // bytes per block image (3 parts x 32 rows x 32 B)
+struct RespB16 {
+    static constexpr int NS = D / 32, CT = D / 16;
+    static constexpr int NB = CT == 8 ? 20 : 6;     // sum over ct of ct / 2 + 1
+    static constexpr int BLK = 3 * 1024;
+    static constexpr int NW = 8, NU = 2;
+    static constexpr int UB = NB / NU, UBYTES = UB * BLK;
+    static constexpr int PAR = 2 * UBYTES, PARF = 256 + 64;
+    static constexpr int LDS_BYTES = PAR + 2 * PARF * 4;
+    static constexpr int PIECES = UBYTES / 1024;
     int ct[NB], s[NB];
-    constexpr RespBf3() : ct(), s() {
+    constexpr RespB16() : ct(), s() {
         int n = 0;
         for (int c = 0; c < CT; ++c)
-            for (int k = 0; k <= 2 * c + 1; ++k) {
+            for (int k = 0; k <= c / 2; ++k) {
                 ct[n] = c;
                 s[n] = k;
                 ++n;
             }
     }
-    // byte offset in a block image of (part P, row i, 16-B granule g): two granules per 32-B row,
-    // swapped on rows with bit 4 set (the lane groups of ds_read_b128 then hit 16 distinct 4-bank
-    // groups)
     __host__ __device__ static constexpr int at(int P, int i, int g) {
-        return P * 1024 + i * 32 + 16 * (g ^ ((i >> 4) & 1));
+        return P * 1024 + i * 64 + 16 * (g ^ (((i >> 2) & 1) << 1));
     }
 };
 
-template <int D, int NW, int NU>
-struct RespBf3Shape {
-    static constexpr int NB = RespBf3<D>::NB;
-    // (NU even: unit t's buffer is t & 1 = u & 1, and component k + 1's parameters, staged with
-    // its first unit, never land in the buffer component k's epilogue is reading)
-    static_assert(NB % NU == 0 && NU % 2 == 0, "whole blocks per unit, an even unit count");
-    static constexpr int UB = NB / NU;                      // blocks per unit
-    static constexpr int UBYTES = UB * RespBf3<D>::BLK;
-    static constexpr int PAR = 2 * UBYTES;                  // par[2][256 + 64] floats: mu_k P_k, log_norm_k
-    static constexpr int PARF = 256 + 64;
-    static constexpr int LDS_BYTES = PAR + 2 * PARF * 4;
-    static constexpr int PIECES = UBYTES / 1024;
-};
-
-// the product shape: 4 wavefronts x 32 rows, two units of 10 blocks per component at d = 128, A
-// parts read one block ahead (4.54 ms vs 4.58-4.61 with four units and no read-ahead,
-// profiles/r06_ab_estep_bf3.txt; A/B hooks below)
-#ifndef COME_RESP3_NW
-#define COME_RESP3_NW 4
-#endif
-#ifndef COME_RESP3_NU
-#define COME_RESP3_NU 2
-#endif
-#ifndef COME_RESP3_PF
-#define COME_RESP3_PF 1
-#endif
 template <int D>
-struct RespBf3Pick {
-    static constexpr int NW = COME_RESP3_NW;
-    static constexpr int NU = D == 64 ? 2 : COME_RESP3_NU;
-    using S = RespBf3Shape<D, NW, NU>;
-};
-
-// prec_chol [K][D][D] (upper) -> per component the NB block images of P_k^T's parts, block order
-// of RespBf3 (thread: one block row i and granule g = 8 consecutive features)
-template <int D>
-__global__ void __launch_bounds__(256) k_pack_upper_bf3(const float *__restrict__ P,
+__global__ void __launch_bounds__(256) k_pack_upper_b16(const float *__restrict__ P,
                                                         char *__restrict__ img, int K) {
-    using R = RespBf3<D>;
+    using R = RespB16<D>;
     constexpr R TB{};
-    const int64_t n = (int64_t)K * R::NB * 32 * 2;
+    const int64_t n = (int64_t)K * R::NB * 16 * 4;
     for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n;
          t += (int64_t)gridDim.x * 256) {
-        const int g = (int)(t & 1), i = (int)((t >> 1) & 31);
+        const int g = (int)(t & 3), i = (int)((t >> 2) & 15);
         const int64_t kb = t >> 6;  // k * NB + block
         const int b = (int)(kb % R::NB);
         const int64_t k = kb / R::NB;
-        const int c = 32 * TB.ct[b] + i, f0 = 16 * TB.s[b] + 8 * g;
+        const int c = 16 * TB.ct[b] + i, f0 = 32 * TB.s[b] + 8 * g;
         const float *Pk = P + k * D * D;
         float v[8];
 #pragma unroll
@@ -1175,40 +1148,11 @@ __global__ void __launch_bounds__(256) k_pack_upper_bf3(const float *__restrict_
     }
 }
 
-// unit t (component t / NU, unit t % NU) -> buffer b; with a component's first unit also its
-// mu_k P_k and log_norm_k -> par buffer k & 1
-template <int D, int NW, int NU>
-__device__ __forceinline__ void respbf3_stage(const RespArgs &a, const char *gimg, int64_t t,
-                                              char *smb, int b, int wid, int lane) {
-    using S = RespBf3Shape<D, NW, NU>;
-    const char *src = gimg + t * S::UBYTES + 16 * lane;
-#pragma unroll
-    for (int j = 0; j < (S::PIECES + NW - 1) / NW; ++j) {
-        const int i = wid + NW * j;
-        if (S::PIECES % NW != 0 && i >= S::PIECES) break;  // wavefront-uniform
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const float *>(src + i * 1024),
-                                         reinterpret_cast<float *>(smb + b * S::UBYTES + i * 1024),
-                                         16, 0, 0);
-    }
-    if (t % NU == 0) {
-        const int64_t k = t / NU;
-        float *par = reinterpret_cast<float *>(smb + S::PAR) + (k & 1) * S::PARF;
-        if (wid == 0) {
-            const int s = lane * 4 < D ? lane * 4 : D - 4;
-            __builtin_amdgcn_global_load_lds(a.mu_prec + k * D + s, par, 16, 0, 0);
-        } else if (wid == 1) {
-            __builtin_amdgcn_global_load_lds(a.log_norm + k, par + 256, 4, 0, 0);
-        }
-    }
-}
-
-template <int D, int NW, int NU>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
-    k_gmm_resp_bf3(RespArgs a) {
-    using R = RespBf3<D>;
-    using S = RespBf3Shape<D, NW, NU>;
+template <int D>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+    k_gmm_resp_b16(RespArgs a) {
+    using R = RespB16<D>;
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    using f32x16 = __attribute__((ext_vector_type(16))) float;
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
     extern __shared__ __attribute__((aligned(16))) char smb[];
     if (__builtin_amdgcn_readfirstlane(a.lower[a.K]) != 0) return;
@@ -1216,13 +1160,35 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     const char *gimg = reinterpret_cast<const char *>(a.prec_t);
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int j = lane & 31, h = lane >> 5;
-    const int64_t row = (int64_t)blockIdx.x * (32 * NW) + wid * 32 + j;
+    const int j = lane & 15, kg = lane >> 4;
+    const int64_t row = (int64_t)blockIdx.x * 128 + wid * 16 + j;
     const bool rowok = row < a.V;
-    const int nt = a.K * NU;
-    respbf3_stage<D, NW, NU>(a, gimg, 0, smb, 0, wid, lane);
-    if (nt > 1) respbf3_stage<D, NW, NU>(a, gimg, 1, smb, 1, wid, lane);
-    // the row's parts, once: xp[s][P] = part P of features 16 s + 8 h .. + 7
+    const int nt = a.K * R::NU;
+    // unit t -> buffer b; a component's first unit also brings its mu_k P_k and log_norm_k
+    auto stage = [&](int64_t t, int b) {
+        const char *src = gimg + t * R::UBYTES + 16 * lane;
+#pragma unroll
+        for (int q = 0; q < (R::PIECES + R::NW - 1) / R::NW; ++q) {
+            const int i = wid + R::NW * q;
+            if (R::PIECES % R::NW != 0 && i >= R::PIECES) break;  // wavefront-uniform
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const float *>(src + i * 1024),
+                                             reinterpret_cast<float *>(smb + b * R::UBYTES + i * 1024),
+                                             16, 0, 0);
+        }
+        if (t % R::NU == 0) {
+            const int64_t k = t / R::NU;
+            float *par = reinterpret_cast<float *>(smb + R::PAR) + (k & 1) * R::PARF;
+            if (wid == 0) {
+                const int s = lane * 4 < D ? lane * 4 : D - 4;
+                __builtin_amdgcn_global_load_lds(a.mu_prec + k * D + s, par, 16, 0, 0);
+            } else if (wid == 1) {
+                __builtin_amdgcn_global_load_lds(a.log_norm + k, par + 256, 4, 0, 0);
+            }
+        }
+    };
+    stage(0, 0);
+    if (nt > 1) stage(1, 1);
+    // the row's parts, once: xp[s][P] = part P of features 32 s + 8 kg .. + 7
     bf16x8 xp[R::NS][3];
 #pragma unroll
     for (int s = 0; s < R::NS; ++s) {
@@ -1230,7 +1196,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            if (rowok) v = *reinterpret_cast<const f32x4 *>(a.x + row * D + 16 * s + 8 * h + 4 * u);
+            if (rowok) v = *reinterpret_cast<const f32x4 *>(a.x + row * D + 32 * s + 8 * kg + 4 * u);
             bf16_split3(v[0], v[1], w[0][2 * u], w[1][2 * u], w[2][2 * u]);
             bf16_split3(v[2], v[3], w[0][2 * u + 1], w[1][2 * u + 1], w[2][2 * u + 1]);
         }
@@ -1238,108 +1204,50 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
         for (int P = 0; P < 3; ++P)
             xp[s][P] = __builtin_bit_cast(bf16x8, uint4{w[P][0], w[P][1], w[P][2], w[P][3]});
     }
-    const int aoff = R::at(0, j, h);
+    const int aoff = R::at(0, j, kg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const bool owner = h == 0 && rowok;
+    const bool owner = kg == 0 && rowok;
     float run_max = -INFINITY, run_sum = 0.0f, lp_prev = 0.0f;
     for (int k = 0; k < a.K; ++k) {
-        // component k - 1's log-probability stored one component late (k_gmm_resp16t's reason)
-        if (k > 0 && owner) a.resp[row * a.K + k - 1] = lp_prev;
-        // sum over the row's columns of (Y - mu_k P_k)^2, tile by tile as each tile's last block
-        // completes (the VALU of tile ct beside the MFMAs of ct + 1): register r of tile ct is
-        // column 32 ct + (r & 3) + 8 (r >> 2) + 4 h
-        const float *par = reinterpret_cast<const float *>(smb + S::PAR) + (k & 1) * S::PARF;
+        if (k > 0 && owner) a.resp[row * a.K + k - 1] = lp_prev;  // one component late
+        const float *par = reinterpret_cast<const float *>(smb + R::PAR) + (k & 1) * R::PARF;
         float sq = 0.0f;
-        f32x16 acc[R::CT];
-        auto tile_sq = [&](int ct) {  // tile ct's squared residuals into sq
+        f32x4 acc[R::CT];
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const f32x4 mp = *reinterpret_cast<const f32x4 *>(par + 32 * ct + 8 * g4 + 4 * h);
+        for (int u = 0; u < R::NU; ++u) {
+            const int t = k * R::NU + u;
+            const char *ub = smb + (u & 1) * R::UBYTES;  // t & 1
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float y = acc[ct][4 * g4 + e] - mp[e];
-                    sq = __builtin_fmaf(y, y, sq);
-                }
-            }
-        };
-#if COME_RESP3_PF
-        // A parts read one block ahead, each into the register its predecessor frees (A3 after
-        // the block's first MFMA, A2 after the third, A1 after the sixth), and a finished tile's
-        // squares taken after the next block's third MFMA (its accumulator is then complete
-        // and no MFMA of this wavefront waits on the VALU)
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int t = k * NU + u;
-            const char *ub = smb + (u & 1) * S::UBYTES;  // t & 1
-            auto ld = [&](int bi, int P) {
-                return *reinterpret_cast<const bf16x8 *>(ub + bi * R::BLK + aoff + P * 1024);
-            };
-            bf16x8 A[3];
-            A[2] = ld(0, 2);
-            A[1] = ld(0, 1);
-            A[0] = ld(0, 0);
-#pragma unroll
-            for (int bi = 0; bi < S::UB; ++bi) {
-                const int b = u * S::UB + bi, ct = TB.ct[b], s = TB.s[b];
-                const bool nx = bi + 1 < S::UB;
-                const f32x16 c0 = s == 0 ? f32x16{} : acc[ct];
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], xp[s][0], c0, 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (nx) A[2] = ld(bi + 1, 2);
-                __builtin_amdgcn_sched_barrier(0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][1], acc[ct], 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][0], acc[ct], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (nx) A[1] = ld(bi + 1, 1);
-                __builtin_amdgcn_sched_barrier(0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][2], acc[ct], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (b > 0 && TB.s[b - 1] == 2 * TB.ct[b - 1] + 1) tile_sq(TB.ct[b - 1]);
-                __builtin_amdgcn_sched_barrier(0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][1], acc[ct], 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][0], acc[ct], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (nx) A[0] = ld(bi + 1, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (t + 1 < nt) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();  // buffer t & 1 free; unit t + 1 (and its parameters) in LDS
-                if (t + 2 < nt) respbf3_stage<D, NW, NU>(a, gimg, t + 2, smb, u & 1, wid, lane);
-            }
-        }
-        tile_sq(R::CT - 1);
-#else
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int t = k * NU + u;
-            const char *ub = smb + (u & 1) * S::UBYTES;  // t & 1
-#pragma unroll
-            for (int bi = 0; bi < S::UB; ++bi) {
-                const int b = u * S::UB + bi, ct = TB.ct[b], s = TB.s[b];
+            for (int bi = 0; bi < R::UB; ++bi) {
+                const int b = u * R::UB + bi, ct = TB.ct[b], s = TB.s[b];
                 const char *base = ub + bi * R::BLK + aoff;
                 bf16x8 A[3];
 #pragma unroll
                 for (int P = 0; P < 3; ++P) A[P] = *reinterpret_cast<const bf16x8 *>(base + P * 1024);
-                // a tile's first block starts from the constant 0 (no accumulator reset)
-                const f32x16 c0 = s == 0 ? f32x16{} : acc[ct];
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], xp[s][0], c0, 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][1], acc[ct], 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][2], acc[ct], 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], xp[s][0], acc[ct], 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][1], acc[ct], 0, 0, 0);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], xp[s][0], acc[ct], 0, 0, 0);
-                if (s == 2 * ct + 1) tile_sq(ct);  // tile ct complete
+                const f32x4 c0 = s == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : acc[ct];
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], xp[s][0], c0, 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], xp[s][1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], xp[s][2], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], xp[s][0], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], xp[s][1], acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], xp[s][0], acc[ct], 0, 0, 0);
+                if (s == ct / 2) {  // tile ct complete: columns 16 ct + 4 kg + r
+                    const f32x4 mp = *reinterpret_cast<const f32x4 *>(par + 16 * ct + 4 * kg);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float y = acc[ct][r] - mp[r];
+                        sq = __builtin_fmaf(y, y, sq);
+                    }
+                }
             }
             if (t + 1 < nt) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();  // buffer t & 1 free; unit t + 1 (and its parameters) in LDS
-                if (t + 2 < nt) respbf3_stage<D, NW, NU>(a, gimg, t + 2, smb, u & 1, wid, lane);
+                if (t + 2 < nt) stage(t + 2, u & 1);
             }
         }
-#endif
-        const float lp = par[256] - 0.5f * reduce_stage<5>(sq);
+        const float lp = par[256] - 0.5f * reduce_stage<5>(reduce_stage<4>(sq));
         lse_push(lp, run_max, run_sum);
         lp_prev = lp;
     }
@@ -2258,39 +2166,34 @@ extern "C" int come_gmm_estep(const float *x, int64_t V, int d, const float *pre
         a.prec_t = pt;
         const int r16 = current_opts().gmm_resp16;
         if (r16 == 3) {
-            // default: k_gmm_resp_bf3 over the bf16-part images of the upper factors, then
+            // default: k_gmm_resp_b16 over the bf16-part images of the upper factors, then
             // k_gmm_resp16_full (a no-op unless some factor is lower or dense)
-            using P64 = RespBf3Pick<64>;
-            using P128 = RespBf3Pick<128>;
-            const size_t img_bytes = (size_t)K * (d == 64 ? RespBf3<64>::NB : RespBf3<128>::NB) *
-                                     RespBf3<64>::BLK;
+            const size_t img_bytes =
+                (size_t)K * (d == 64 ? RespB16<64>::NB : RespB16<128>::NB) * RespB16<64>::BLK;
             char *img = (char *)stream_scratch(dev, stream, kScratchRespSplit, img_bytes);
             if (!img) return scratch_failed();
-            const int64_t work = (int64_t)K * (d == 64 ? RespBf3<64>::NB : RespBf3<128>::NB) * 64;
-            hipLaunchKernelGGL(d == 64 ? k_pack_upper_bf3<64> : k_pack_upper_bf3<128>,
+            const int64_t work = (int64_t)K * (d == 64 ? RespB16<64>::NB : RespB16<128>::NB) * 64;
+            hipLaunchKernelGGL(d == 64 ? k_pack_upper_b16<64> : k_pack_upper_b16<128>,
                                dim3((unsigned)std::min<int64_t>((work + 255) / 256, 4096)),
                                dim3(256), 0, (hipStream_t)stream, prec_chol, img, K);
-            rc = hip_error(hipGetLastError(), "k_pack_upper_bf3 launch");
+            rc = hip_error(hipGetLastError(), "k_pack_upper_b16 launch");
             if (rc) return rc;
             RespArgs b = a;
             b.prec_full = a.prec_t;
             b.prec_t = reinterpret_cast<const float *>(img);
-            void (*kern)(RespArgs) = d == 64 ? k_gmm_resp_bf3<64, P64::NW, P64::NU>
-                                             : k_gmm_resp_bf3<128, P128::NW, P128::NU>;
             static bool attr3 = false;
             if (!attr3) {
-                for (void (*f)(RespArgs) : {k_gmm_resp_bf3<64, P64::NW, P64::NU>,
-                                            k_gmm_resp_bf3<128, P128::NW, P128::NU>,
+                for (void (*f)(RespArgs) : {k_gmm_resp_b16<64>, k_gmm_resp_b16<128>,
                                             k_gmm_resp16_full<64>, k_gmm_resp16_full<128>})
                     (void)hipFuncSetAttribute((const void *)f,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr3 = true;
             }
-            const int nw = d == 64 ? P64::NW : P128::NW;
-            hipLaunchKernelGGL(kern, dim3((unsigned)((V + 32 * nw - 1) / (32 * nw))), dim3(64 * nw),
-                               d == 64 ? P64::S::LDS_BYTES : P128::S::LDS_BYTES, (hipStream_t)stream,
-                               b);
-            rc = hip_error(hipGetLastError(), "k_gmm_resp_bf3 launch");
+            hipLaunchKernelGGL(d == 64 ? k_gmm_resp_b16<64> : k_gmm_resp_b16<128>,
+                               dim3((unsigned)((V + 127) / 128)), dim3(512),
+                               d == 64 ? RespB16<64>::LDS_BYTES : RespB16<128>::LDS_BYTES,
+                               (hipStream_t)stream, b);
+            rc = hip_error(hipGetLastError(), "k_gmm_resp_b16 launch");
             if (rc) return rc;
             const size_t lds16 = sizeof(float) * (size_t)(d == 64 ? Resp16Shape<64>::LDS
                                                                    : Resp16Shape<128>::LDS);

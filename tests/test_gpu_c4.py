@@ -132,7 +132,7 @@ def test_c4_responsibilities_k50_1m(c4_rows, r16):
 
 
 def test_c4_estep_bf3_error_is_fp32_level(c4_rows):
-    """k_gmm_resp_bf3's per-row log-sum-exp (the EM log-likelihood term) against float64 on 100k
+    """k_gmm_resp_b16's per-row log-sum-exp (the EM log-likelihood term) against float64 on 100k
     C4 rows: RMS and max error within 1.5x of the fp32-MFMA E-step's (k_gmm_resp16t) -- the
     bf16-part products are not a reduced-precision form (see the community test above)."""
     from come_amd import _lib

@@ -86,7 +86,7 @@ def test_estep_mixed_factor_shapes(d, r16):
     """The MFMA E-step skips the zero blocks of upper-triangular factors only: components with a
     lower factor (sklearn's cholesky(precisions_init, lower=True)) or a dense factor run the full
     loop.  Mixed in one launch, every component must match the float64 quadratic form -- for the
-    bf16-part k_gmm_resp_bf3 (gmm_resp16 = 3) and the fp32 k_gmm_resp16t (= 2): a lower or dense
+    bf16-part k_gmm_resp_b16 (gmm_resp16 = 3) and the fp32 k_gmm_resp16t (= 2): a lower or dense
     factor in the launch sends every component to the separate k_gmm_resp16_full launch."""
     V, K = 1500, 6
     rng = np.random.RandomState(d)
@@ -115,7 +115,7 @@ def test_estep_mixed_factor_shapes(d, r16):
 @pytest.mark.parametrize("V,K,d", [(4097, 50, 128), (70_001, 7, 64), (300, 3, 64), (129, 1, 128),
                                    (1, 4, 128), (5000, 2, 128)])
 def test_estep_default_and_fallback_agree(V, K, d):
-    """The E-step forms -- k_gmm_resp_bf3 (bf16 parts) and k_gmm_resp16t (16-wide fp32 blocks) --
+    """The E-step forms -- k_gmm_resp_b16 (bf16 parts) and k_gmm_resp16t (16-wide fp32 blocks) --
     on sklearn-shaped upper factors, ragged row counts: the same quantities summed in different
     orders, equal to float tolerance, responsibilities summing to 1."""
     rng = np.random.RandomState(V + 7 * K)
@@ -315,7 +315,7 @@ def test_community2vec_trains_at_d256():
                                    (129, 1, 128)])
 @pytest.mark.parametrize("r16", [2, 3])
 def test_estep_upper_factors_vs_float64(V, K, d, r16):
-    """k_gmm_resp_bf3 (gmm_resp16 = 3) and k_gmm_resp16t (= 2) with
+    """k_gmm_resp_b16 (gmm_resp16 = 3) and k_gmm_resp16t (= 2) with
     sklearn-shaped (upper-triangular) precision factors only -- the launches that take the
     triangular skip -- against the float64 quadratic form, ragged rows."""
     from scipy.special import logsumexp
