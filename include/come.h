@@ -278,7 +278,7 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       11.5 ms).  Other values: COME_E_INVALID
  *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 4 = k_gmm_cov_bf3 (E^T E with
  *                       E = sqrt(r) (x - m) carried as three bf16 parts, six exact part products
- *                       per multiply-add on 32x32x16 bf16 MFMAs, 10 upper 32x32 tiles; 5.62 ms at
+ *                       per multiply-add on 32x32x16 bf16 MFMAs, 10 upper 32x32 tiles; 5.3 ms at
  *                       C4); 3 = k_gmm_cov16 (fp32 16x16x4 tiles: 36 of 64 upper tiles at d =
  *                       128; 7.22 ms).  Other values: COME_E_INVALID
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);

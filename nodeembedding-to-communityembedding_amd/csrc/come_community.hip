@@ -46,6 +46,14 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #ifndef COME_COV_NS
 #define COME_COV_NS 4
 #endif
+// k_gmm_cov_bf3 at d = 128: staging wavefronts per workgroup (8: 5.32-5.35 vs 5.49-5.50 ms with 4,
+// profiles/r06_ab_scatter_bf3.txt) and staging register sets (A/B hooks)
+#ifndef COME_COV3_SW
+#define COME_COV3_SW 8
+#endif
+#ifndef COME_COV3_NS
+#define COME_COV3_NS 3
+#endif
 constexpr int kThreads = 256;
 
 // out[r][c] = sum_j A[r][j] * B(c, j) for the tile, where B(c, j) = Bm[c*d + j] (TRANS=false,
@@ -1642,14 +1650,16 @@ struct CovBf3 {
     static constexpr int CPW = D == 128 ? 2 : 4;    // components per workgroup
     static constexpr int WPC = D == 128 ? 2 : 1;    // MFMA wavefronts per component
     static constexpr int AW = CPW * WPC;            // MFMA wavefronts (4)
-    static constexpr int THREADS = 64 * (AW + 4);   // + 4 staging wavefronts
+    static constexpr int SW = D == 128 ? COME_COV3_SW : 4;  // staging wavefronts
+    static constexpr int THREADS = 64 * (AW + SW);
     static constexpr int NTW = D == 128 ? 5 : 3;    // tiles per MFMA wavefront
     static constexpr int NF = D / 32;               // fragments (32-feature row groups)
     static constexpr int PLANE = D * RB * 2;        // bytes per part image (D rows x 32 bf16)
     static constexpr int IMG = 3 * PLANE;           // per component (24 KB at d = 128)
     static constexpr int BUF = CPW * IMG;
     static constexpr int LDS_BYTES = 2 * BUF;       // 96 KB: one workgroup per CU
-    static constexpr int SPT = RB * D / 256;        // samples per staging thread (16 / 8)
+    static constexpr int SPT = RB * D / (64 * SW);  // samples per staging thread (16 / 8)
+    static_assert(SPT % 8 == 0, "a staging thread fills whole 8-sample granules");
     // granule swizzle: bit 0 = bit 2 of the row, bit 1 = bit 1 ^ bit 3 -- distinct over the rows
     // of every 16-lane ds_read_b128 group (64 banks) and of every 8-lane ds_write_b128 group (32
     // banks: 8 consecutive rows) that share a bank column
@@ -1749,7 +1759,7 @@ template <int D>
 struct CovBf3Stage {
     using C = CovBf3<D>;
     static constexpr int SPT = C::SPT, CPW = C::CPW;
-    static constexpr int NS = 3;  // register sets: loads run NS blocks ahead
+    static constexpr int NS = COME_COV3_NS;  // register sets: loads run NS blocks ahead
     const CovArgs &a;
     const int f, sg, k0, nk, lane;
     const int64_t c0, c1;
