@@ -54,6 +54,10 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #ifndef COME_COV3_NS
 #define COME_COV3_NS 3
 #endif
+// MFMA wavefronts per d = 128 component (4: 5.50 vs 5.42-5.44 ms with 2, r06zl)
+#ifndef COME_COV3_WPC
+#define COME_COV3_WPC 2
+#endif
 constexpr int kThreads = 256;
 
 // out[r][c] = sum_j A[r][j] * B(c, j) for the tile, where B(c, j) = Bm[c*d + j] (TRANS=false,
@@ -1648,11 +1652,10 @@ template <int D>
 struct CovBf3 {
     static constexpr int RB = 32;                   // samples per block (2 k-steps)
     static constexpr int CPW = D == 128 ? 2 : 4;    // components per workgroup
-    static constexpr int WPC = D == 128 ? 2 : 1;    // MFMA wavefronts per component
+    static constexpr int WPC = D == 128 ? COME_COV3_WPC : 1;  // MFMA wavefronts per component
     static constexpr int AW = CPW * WPC;            // MFMA wavefronts (4)
     static constexpr int SW = D == 128 ? COME_COV3_SW : 4;  // staging wavefronts
     static constexpr int THREADS = 64 * (AW + SW);
-    static constexpr int NTW = D == 128 ? 5 : 3;    // tiles per MFMA wavefront
     static constexpr int NF = D / 32;               // fragments (32-feature row groups)
     static constexpr int PLANE = D * RB * 2;        // bytes per part image (D rows x 32 bf16)
     static constexpr int IMG = 3 * PLANE;           // per component (24 KB at d = 128)
@@ -1674,23 +1677,38 @@ struct CovBf3 {
 // tile n of MFMA part p: (row group ta, column group tb), ta <= tb
 template <int D>
 struct CovBf3Tiles {
-    int ta[2][5], tb[2][5];
-    constexpr CovBf3Tiles() : ta(), tb() {
-        if (D == 128) {
-            const int a0[5] = {0, 0, 0, 0, 3}, b0[5] = {0, 1, 2, 3, 3};
-            const int a1[5] = {1, 1, 1, 2, 2}, b1[5] = {1, 2, 3, 2, 3};
-            for (int n = 0; n < 5; ++n) {
-                ta[0][n] = a0[n];
-                tb[0][n] = b0[n];
-                ta[1][n] = a1[n];
-                tb[1][n] = b1[n];
+    static constexpr int WPC = CovBf3<D>::WPC;
+    int cnt[4], ta[4][5], tb[4][5];
+    bool need[4][4];  // fragments a part reads
+    constexpr CovBf3Tiles() : cnt(), ta(), tb(), need() {
+        // d = 128: 10 upper tiles per component, 5 / 5 over 2 wavefronts or 3 / 3 / 2 / 2 over 4
+        const int a2[2][5] = {{0, 0, 0, 0, 3}, {1, 1, 1, 2, 2}};
+        const int b2[2][5] = {{0, 1, 2, 3, 3}, {1, 2, 3, 2, 3}};
+        const int a4[4][3] = {{0, 0, 0}, {0, 1, 3}, {1, 1, 0}, {2, 2, 0}};
+        const int b4[4][3] = {{0, 1, 2}, {3, 3, 3}, {1, 2, 0}, {2, 3, 0}};
+        const int c4[4] = {3, 3, 2, 2};
+        for (int p = 0; p < 4; ++p) {
+            if (D == 128 && WPC == 2 && p < 2) {
+                cnt[p] = 5;
+                for (int n = 0; n < 5; ++n) {
+                    ta[p][n] = a2[p][n];
+                    tb[p][n] = b2[p][n];
+                }
+            } else if (D == 128 && WPC == 4) {
+                cnt[p] = c4[p];
+                for (int n = 0; n < c4[p]; ++n) {
+                    ta[p][n] = a4[p][n];
+                    tb[p][n] = b4[p][n];
+                }
+            } else if (D == 64 && p == 0) {
+                const int a0[3] = {0, 0, 1}, b0[3] = {0, 1, 1};
+                cnt[p] = 3;
+                for (int n = 0; n < 3; ++n) {
+                    ta[p][n] = a0[n];
+                    tb[p][n] = b0[n];
+                }
             }
-        } else {
-            const int a0[3] = {0, 0, 1}, b0[3] = {0, 1, 1};
-            for (int n = 0; n < 3; ++n) {
-                ta[0][n] = a0[n];
-                tb[0][n] = b0[n];
-            }
+            for (int n = 0; n < cnt[p]; ++n) need[p][ta[p][n]] = need[p][tb[p][n]] = true;
         }
     }
 };
@@ -1702,14 +1720,13 @@ __device__ __forceinline__ void covbf3_part(const CovArgs &a, const char *smb, i
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
     constexpr CovBf3Tiles<D> TT{};
+    constexpr int NT = TT.cnt[P];
     const int i = lane & 31, h = lane >> 5;
-    f32x16 acc[C::NTW];
+    f32x16 acc[NT];
 #pragma unroll
-    for (int n = 0; n < C::NTW; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[n][e] = 0.0f;
-    // which fragments this part reads (part 1 of d = 128 never needs fragment 0)
-    constexpr bool need0 = !(D == 128 && P == 1);
     for (int j = 0; j < nb; ++j) {
         __syncthreads();  // barrier j: block j staged
         const char *im = smb + (j & 1) * C::BUF + tk * C::IMG;
@@ -1718,13 +1735,13 @@ __device__ __forceinline__ void covbf3_part(const CovArgs &a, const char *smb, i
             bf16x8 F[C::NF][3];
 #pragma unroll
             for (int f = 0; f < C::NF; ++f) {
-                if (f == 0 && !need0) continue;
+                if (!TT.need[P][f]) continue;
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
                     F[f][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * f + i, 2 * st + h));
             }
 #pragma unroll
-            for (int n = 0; n < C::NTW; ++n) {
+            for (int n = 0; n < NT; ++n) {
                 const int ta = TT.ta[P][n], tb = TT.tb[P][n];
                 acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][2], F[tb][0], acc[n], 0, 0, 0);
                 acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
@@ -1738,7 +1755,7 @@ __device__ __forceinline__ void covbf3_part(const CovArgs &a, const char *smb, i
     if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
     float *out = a.out + (chunk * a.K + k0 + tk) * D * D;
 #pragma unroll
-    for (int n = 0; n < C::NTW; ++n) {
+    for (int n = 0; n < NT; ++n) {
         const int ta = TT.ta[P][n], tb = TT.tb[P][n];
         const int jj = 32 * tb + i;
 #pragma unroll
@@ -1833,9 +1850,14 @@ __global__ void __launch_bounds__(CovBf3<D>::THREADS) __attribute__((amdgpu_wave
     const int nb = c1 > c0 ? (int)((c1 - c0 + C::RB - 1) / C::RB) : 0;
     const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     if (wid < C::AW) {
-        const int tk = wid / C::WPC, p = wid % C::WPC;
+        // wavefronts w and w + 4 share a SIMD: with 4 parts per component, component 1's part
+        // index is shifted by 2 so that each SIMD gets 3 + 2 tiles
+        const int tk = wid / C::WPC;
+        const int p = C::WPC == 4 ? (wid % 4 + 2 * tk) % 4 : wid % C::WPC;
         if (p == 0) covbf3_part<D, 0>(a, smb, nb, tk, nk, k0, chunk, lane);
-        else covbf3_part<D, (C::WPC > 1 ? 1 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else if (p == 1) covbf3_part<D, (C::WPC > 1 ? 1 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else if (p == 2) covbf3_part<D, (C::WPC > 2 ? 2 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else covbf3_part<D, (C::WPC > 2 ? 3 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
         return;
     }
     CovBf3Stage<D> sg(a, tid - 64 * C::AW, lane, k0, nk, c0, c1);
