@@ -116,6 +116,7 @@ def secondary_rows(timeout_s=150):
                     row["traffic_GBps"] = rf["traffic"] / (rf["avg_kernel_ms"] / 1e3) / 1e9
             if wl == "c4":
                 row["community_kernel"] = j["config"]["community_kernel"]
+                row["arithmetic"] = j["config"].get("arithmetic")
                 row["roofline_peak"] = j["roofline"]["peak"]
                 row["roofline_peak_basis"] = j["roofline"].get("peak_basis")
                 row["frac_of_fp32_mfma_peak"] = j["roofline"].get("frac_of_fp32_mfma_peak")

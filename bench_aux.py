@@ -274,6 +274,11 @@ def c4(args):
         "higher_is_better": True, "dtype": "f32", "data": "synthetic N(0,1) rows, random SPD",
         "config": {"workload": "configs[3]/C4: V=%d K=%d d=%d" % (V, K, d),
                    "community_kernel": comm_kernel,
+                   # what "f32" means for the bf16-part kernels (README)
+                   "arithmetic": ("fp32 operands as three bf16 parts, six exact part products per "
+                                  "multiply-add on bf16 MFMAs, fp32 accumulation; error vs "
+                                  "float64 at the fp32 kernels' level (tests/test_gpu_c4.py)")
+                                 if comm_bf3 else "fp32 MFMA (exact fp32 products)",
                    # E-step / scatter: 2 V K d^2 algorithmic flops, of which the kernels execute
                    # only the upper-triangular / symmetric blocks (fractions above)
                    "gmm_resp_kernel": resp_kernel, "gmm_resp_blocks_executed": tri_resp,
