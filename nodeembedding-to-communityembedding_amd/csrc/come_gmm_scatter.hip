@@ -1,0 +1,762 @@
+// come_gmm_scatter.hip -- GMM M-step scatter matrices (gfx950).
+//
+// Replaces the numerator of sklearn's _estimate_gaussian_covariances_full (community_embeddings.py
+// :27 fit): come_gmm_scatter -> k_gmm_cov_bf3 (default, fp32 operands as bf16 parts), k_gmm_cov16
+// (fp32 MFMA), k_gmm_cov_valu / k_gmm_cov_wide (VALU, any d), k_gmm_cov_reduce (chunk partials in a
+// fixed order).
+
+#include "come_c4.h"
+
+namespace come {
+
+// ---- GMM M-step scatter matrices -------------------------------------------------------------
+//
+// S_k = sum_i resp[i,k] (x_i - mu_k)(x_i - mu_k)^T, the numerator of sklearn's full covariance
+// (_estimate_gaussian_covariances_full: np.dot(resp[:, k] * diff.T, diff) / nk[k]), 2 V K d^2
+// flops per M-step.  Workgroup (k, chunk): rows of the chunk are staged through LDS in blocks of
+// kCovRB samples, centred on mu_k, with their weights; the reduction over samples is the MFMA
+// k-dimension (v_mfma_f32_32x32x2_f32: lane (r, h) supplies A[c1 = rt*32 + r][sample s0 + h] =
+// w * xc and B[sample s0 + h][c2 = ct*32 + r] = xc).  The D x D output is split into 32 x 32
+// tiles over the 4 wavefronts.  Each chunk writes its own partial; k_gmm_cov_reduce sums the
+// chunks in a fixed order (deterministic, no float atomics).  blockIdx.x = k varies fastest, so
+// the K workgroups of one chunk run together and share its rows through L2 / MALL.
+constexpr int kCovRB = 64;
+
+struct CovArgs {
+    const float *x;
+    const float *resp;
+    const float *means;
+    float *out;  // [chunks][K][d][d] partials (or [K][d][d] when chunks == 1)
+    int64_t V;
+    int64_t rows_per_chunk;
+    int d;
+    int K;
+};
+
+// ---- M-step scatter on v_mfma_f32_16x16x4_f32 (k_gmm_cov16, gmm_cov_async = 3) ----------------
+//
+// 4 MFMA + 4 staging wavefronts, CPW components per workgroup, two image buffers, two workgroups
+// per CU, on 16 x 16 output tiles (only rt <= ct; each off-diagonal tile also stored transposed,
+// so S_k comes out exactly symmetric): the symmetric output needs the
+// 36 upper tiles of 64 at d = 128 (0.5625 of the dense MFMA cycles) instead of 10 of 16 32-wide
+// tiles (0.625).  MFMA (tile rt, ct; 4 samples): A[i][k] = w_s (x_s - mu)[rt*16 + i], B[k][j] =
+// (x_s - mu)[ct*16 + j], lane l: i = j = l % 16, samples s = 16 g + 4 (l / 16) + t for the four
+// steps t of a 16-sample group g, so each operand row of a group is ONE ds_read_b128 of the
+// transposed image B[k][c][s] (rows of 32 samples, 16-byte granules XOR-swizzled by c % 8:
+// conflict-free without padding).  A d = 128 component's 36 tiles split 18 / 18 over two
+// wavefronts by tile rows {0, 1, 6, 7} and {2, 3, 4, 5}; a wavefront weights its 4 A rows once
+// per group and streams the B rows column by column (few VGPRs at 4 waves per SIMD).
+// (Twice the MFMA wavefronts with half the tiles each -- 4 MFMA waves per SIMD, the E-step /
+// community lesson -- was bit-identical and no faster: 7.45 vs 7.35 ms, profiles/r04_ab_scatter16.txt.)
+template <int D>
+struct Cov16 {
+    static constexpr int RB = 32;                 // samples per block
+    static constexpr int LDT = RB;                // image row (swizzled, unpadded)
+    static constexpr int IMG = D * LDT;
+    static constexpr int CPW = D == 128 ? 2 : 4;  // components per workgroup
+    static constexpr int WOFF = CPW * IMG;
+    static constexpr int BUF = CPW * IMG + CPW * RB;
+    static constexpr int NBUF = 2;
+    static constexpr int NT16 = D / 16;
+    static constexpr int WPC = D == 128 ? 2 : 1;                  // MFMA wavefronts per component
+    static constexpr int NTW = NT16 * (NT16 + 1) / 2 / WPC;      // tiles per wavefront
+    static constexpr int NR = 4;                                  // A rows per wavefront
+    static constexpr int AW = CPW * WPC;                          // MFMA wavefronts
+    static constexpr int THREADS = 64 * (AW + 4);                 // + 4 staging wavefronts
+};
+
+// Tiles of MFMA wavefront part p (0 / 1 at d = 128, 0 at d = 64) in issue order (column-major:
+// B row ct once per column), with their A-row slot.
+template <int D>
+struct Cov16Tiles {
+    using C = Cov16<D>;
+    int rows[C::WPC][C::NR];
+    int ct[C::WPC][C::NTW], slot[C::WPC][C::NTW];
+    constexpr Cov16Tiles() : rows(), ct(), slot() {
+        for (int p = 0; p < C::WPC; ++p) {
+            for (int i = 0; i < C::NR; ++i)
+                rows[p][i] = D == 64 ? i : (p == 0 ? (i < 2 ? i : i + 4) : i + 2);
+            int n = 0;
+            for (int c = 0; c < C::NT16; ++c)
+                for (int i = 0; i < C::NR; ++i)
+                    if (rows[p][i] <= c) {
+                        ct[p][n] = c;
+                        slot[p][n] = i;
+                        ++n;
+                    }
+        }
+    }
+};
+
+template <int D>
+__device__ __forceinline__ int cov16_off(int c, int gran) {  // image offset of (row c, granule)
+    return c * Cov16<D>::LDT + 4 * (gran ^ (c & 7));
+}
+
+template <int D, int P>
+__device__ __forceinline__ void cov16_consume(const float *img, int nb, int tk, int lane,
+                                              __attribute__((ext_vector_type(4)))
+                                              float (&acc)[Cov16<D>::NTW]) {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr Cov16Tiles<D> TT{};
+    const int j16 = lane & 15, kg = lane >> 4;
+#if COME_COV_DIAG == 2
+    __syncthreads();
+#endif
+    for (int j = 0; j < nb; ++j) {
+#if COME_COV_DIAG == 2
+        asm volatile("" ::: "memory");  // keep the LDS reads in the loop
+        const float *buf = img;
+#else
+        __syncthreads();  // barrier j: block j staged
+        const float *buf = img + (j % C::NBUF) * C::BUF;
+#endif
+        COME_PRIO(1);
+        const float *im = buf + tk * C::IMG;
+#pragma unroll
+        for (int g = 0; g < C::RB / 16; ++g) {
+            const int gran = 4 * g + kg;
+            const f32x4 w = *reinterpret_cast<const f32x4 *>(buf + C::WOFF + tk * C::RB + 4 * gran);
+            f32x4 wa[C::NR];
+#pragma unroll
+            for (int i = 0; i < C::NR; ++i)
+                wa[i] = w * *reinterpret_cast<const f32x4 *>(
+                                im + cov16_off<D>(TT.rows[P][i] * 16 + j16, gran));
+            f32x4 bv[2];
+            bv[0] = *reinterpret_cast<const f32x4 *>(im + cov16_off<D>(TT.ct[P][0] * 16 + j16, gran));
+            int cur = 0;
+#pragma unroll
+            for (int n = 0; n < C::NTW; ++n) {
+                // the next column's B row, read while this column's MFMAs run
+                if (n + 1 < C::NTW && TT.ct[P][n + 1] != TT.ct[P][n])
+                    bv[cur ^ 1] = *reinterpret_cast<const f32x4 *>(
+                        im + cov16_off<D>(TT.ct[P][n + 1] * 16 + j16, gran));
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[TT.slot[P][n]][t], bv[cur][t],
+                                                                  acc[n], 0, 0, 0);
+                if (n + 1 < C::NTW && TT.ct[P][n + 1] != TT.ct[P][n]) cur ^= 1;
+            }
+        }
+        COME_PRIO(0);
+    }
+}
+
+// the MFMA part of wavefront part P (compile-time tile tables): consume, then store the tiles
+template <int D, int P>
+__device__ __forceinline__ void cov16_part(const CovArgs &a, const float *img, int nb, int tk,
+                                           int nk, int k0, int64_t chunk, int lane) {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    f32x4 acc[C::NTW];
+#pragma unroll
+    for (int n = 0; n < C::NTW; ++n) acc[n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (nb > 0) cov16_consume<D, P>(img, nb, tk, lane, acc);
+    if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+    constexpr Cov16Tiles<D> TT{};
+    const int j16 = lane & 15, kg = lane >> 4;
+    float *out = a.out + (chunk * a.K + k0 + tk) * D * D;
+#pragma unroll
+    for (int n = 0; n < C::NTW; ++n) {
+        const int rt = TT.rows[P][TT.slot[P][n]], ct = TT.ct[P][n];
+        const int jj = ct * 16 + j16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int ii = rt * 16 + 4 * kg + e;
+            out[(int64_t)ii * D + jj] = acc[n][e];
+            if (rt != ct) out[(int64_t)jj * D + ii] = acc[n][e];
+        }
+    }
+}
+
+// k_gmm_cov16's staging wavefronts (256 threads, thread st): block blk of the chunk [c0, c1) goes
+// global -> VGPR register set u (three sets: loads run 3 blocks ahead of the stage that consumes
+// them, an HBM / MALL round trip under load exceeding one block period) -> centred, transposed
+// LDS image per component (stage), with the weights beside it.
+// d = 128: 16-byte loads.  Thread st < RB D / 16 owns feature quad fq = st / 8 (features 4 fq ..
+// 4 fq + 3) of samples 4 sg .. 4 sg + 3, sg = st % 8: one dwordx4 per sample, 8 lanes reading one
+// 128-B line; each feature's 4 samples become one b128 granule (8 consecutive lanes write the 8
+// granules of one image row: conflict-free).  Thread st carries the weight of sample st % RB for
+// component st % (CPW RB) / RB (four threads per weight, the same value: no branch).  (vs one dword per column and sample: 7.27 vs 7.40 ms at C4,
+// bit-identical, profiles/r05_ab_gmm_diag.txt; the d = 64 form below needs too many registers this
+// way: 16 means per thread.)
+template <int D>
+struct Cov16StageX4 {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    static constexpr int RB = C::RB, CPW = C::CPW, NX = RB * D / 16;
+    static_assert(RB == 32 && NX <= 256 && CPW * RB <= 256, "x4 staging layout");
+    const CovArgs &a;
+    const int sg, fq, wk, ws, k0, nk;
+    const bool xl, wlane;
+    const int64_t c0, c1;
+    static constexpr int NS = COME_COV_NS;  // register sets: loads run NS blocks ahead
+    float mu[CPW][4];
+    f32x4 xv[NS][4];
+    float wl[NS];
+    __device__ __forceinline__ Cov16StageX4(const CovArgs &a_, int st, int k0_, int nk_, int64_t c0_,
+                                            int64_t c1_)
+        : a(a_), sg(st % 8), fq(st / 8), wk(st % (CPW * RB) / RB), ws(st % RB), k0(k0_), nk(nk_),
+          xl(st < NX), wlane(true), c0(c0_), c1(c1_) {
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                mu[kk][i] = xl && kk < nk ? a.means[(int64_t)(k0 + kk) * D + 4 * fq + i] : 0.0f;
+    }
+    // Loads are unconditional (rows past the chunk clamped to its last row, components past K
+    // to K - 1) and the out-of-range values zeroed when staged: a load under a divergent branch
+    // leaves the compiler unable to count the loads in flight, and it then waits for all of them
+    // (vmcnt(0)) before every stage -- the three-block lookahead collapses to none.
+    __device__ __forceinline__ void load(int u, int blk) {
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t r = min(b + 4 * sg + t, c1 - 1);
+            xv[u][t] = *reinterpret_cast<const f32x4 *>(a.x + r * D + 4 * fq);
+        }
+        const int64_t wrow = min(b + ws, c1 - 1);
+        wl[u] = a.resp[wrow * a.K + min(k0 + wk, a.K - 1)];
+    }
+    __device__ __forceinline__ void stage(float *img, int u, int blk) const {
+        float *buf = img + (blk % C::NBUF) * C::BUF;
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+        // (the values are read outside any branch: a register read under a divergent branch
+        // also makes the compiler drain every load in flight)
+        const float w = wk < nk && b + ws < c1 ? wl[u] : 0.0f;
+        if (NX == 256 || xl) {  // every thread holds samples at d = 128 (no branch)
+#pragma unroll
+            for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    f32x4 xb;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        xb[t] = b + 4 * sg + t < c1 ? xv[u][t][i] - mu[kk][i] : 0.0f;
+                    *reinterpret_cast<f32x4 *>(buf + kk * C::IMG + cov16_off<D>(4 * fq + i, sg)) = xb;
+                }
+        }
+        buf[C::WOFF + wk * RB + ws] = w;  // (threads st, st + 64, ... write the same value)
+    }
+};
+
+// d = 64: thread owns column sc and samples SPT sp .. SPT sp + SPT
+// - 1 of a block; lane l also carries the weight of sample SPT sp + l % SPT for component
+// l % (SPT CPW) / SPT
+template <int D>
+struct Cov16StageCol {
+    using C = Cov16<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    static constexpr int RB = C::RB, CPW = C::CPW, SPT = RB * D / 256;
+    static_assert(SPT % 4 == 0 && SPT * CPW <= 64 && D % 64 == 0, "staging layout");
+    const CovArgs &a;
+    const int sc, sp, wk, ws, k0, nk;
+    const bool wlane;
+    const int64_t c0, c1;
+    static constexpr int NS = 3;
+    float mu[CPW];
+    float xv[3][SPT];
+    float wl[3];
+    __device__ __forceinline__ Cov16StageCol(const CovArgs &a_, int st, int lane, int k0_, int nk_,
+                                             int64_t c0_, int64_t c1_)
+        : a(a_), sc(st % D), sp(st / D), wk(lane % (SPT * CPW) / SPT), ws(lane % SPT), k0(k0_),
+          nk(nk_), wlane(true), c0(c0_), c1(c1_) {
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+            mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + sc] : 0.0f;
+    }
+    // unconditional loads, out-of-range values zeroed when staged (as Cov16StageX4)
+    __device__ __forceinline__ void load(int u, int blk) {
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) xv[u][q] = a.x[min(b + SPT * sp + q, c1 - 1) * D + sc];
+        const int64_t wrow = min(b + SPT * sp + ws, c1 - 1);
+        wl[u] = a.resp[wrow * a.K + min(k0 + wk, a.K - 1)];
+    }
+    __device__ __forceinline__ void stage(float *img, int u, int blk) const {
+        float *buf = img + (blk % C::NBUF) * C::BUF;
+        const int64_t b = c0 + (COME_COV_DIAG == 3 ? 0 : (int64_t)blk * RB);
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+#pragma unroll
+            for (int j = 0; j < SPT / 4; ++j) {
+                f32x4 xb;
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4)
+                    xb[q4] = b + SPT * sp + 4 * j + q4 < c1 ? xv[u][4 * j + q4] - mu[kk] : 0.0f;
+                *reinterpret_cast<f32x4 *>(buf + kk * C::IMG + cov16_off<D>(sc, (SPT * sp + 4 * j) / 4)) =
+                    xb;
+            }
+        const float w = wk < nk && b + SPT * sp + ws < c1 ? wl[u] : 0.0f;
+        buf[C::WOFF + wk * RB + SPT * sp + ws] = w;  // (lanes l, l + SPT CPW: the same value)
+    }
+};
+
+// the staging pipeline: block j + 1 is staged while block j is multiplied (two image buffers, one
+// barrier per block); register set (j + 1) % NS holds block j + 1, reloaded with block j + 1 + NS.
+// Every load and stage is issued unconditionally (the block index clamped to nb - 1; a stage of
+// block nb lands in a buffer nobody reads again, its values zeroed): with no branch around them
+// the compiler counts the loads in flight exactly and each stage waits only for its own set
+// (a conditional load made it drain all of them, vmcnt(0), at the loop head).
+template <int D, typename S>
+__device__ __forceinline__ void cov16_staging(float *img, S &sg, int nb) {
+    if (nb == 0) return;
+    constexpr int SD = Cov16<D>::NBUF - 1, NS = S::NS;
+    const int last = nb - 1;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) sg.load(u, min(u, last));
+#if COME_COV_DIAG == 2
+    sg.stage(img, 0, 0);
+    __syncthreads();
+    return;
+#endif
+    sg.stage(img, 0, 0);
+    if (COME_COV_DIAG != 1) sg.load(0, min(NS, last));
+    __syncthreads();  // barrier 0
+    for (int j0 = 0; j0 < nb; j0 += NS) {
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {  // j = j0 + u: register set (j + SD) % NS
+            const int j = j0 + u;
+            if (j >= nb) return;  // (not break: the loop head then sees one load order only)
+            sg.stage(img, (u + SD) % NS, j + SD);
+            if (COME_COV_DIAG != 1) sg.load((u + SD) % NS, min(j + SD + NS, last));
+            if (j + 1 < nb) __syncthreads();  // barrier j + 1
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__((Cov16<D>::THREADS))
+    __attribute__((amdgpu_waves_per_eu(4))) k_gmm_cov16(CovArgs a) {
+    using C = Cov16<D>;
+    constexpr int CPW = C::CPW;
+    constexpr int RB = C::RB;
+    static_assert(C::NBUF * C::BUF * sizeof(float) * 2 <= 160 * 1024, "two workgroups per CU");
+    __shared__ __attribute__((aligned(16))) float img[C::NBUF * C::BUF];
+    const int64_t chunk = blockIdx.y;
+    const int k0 = blockIdx.x * CPW;
+    const int nk = a.K - k0 < CPW ? a.K - k0 : CPW;
+    const int64_t c0 = chunk * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int nb = c1 > c0 ? (int)((c1 - c0 + RB - 1) / RB) : 0;
+    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wid < C::AW) {
+        // ---- MFMA wavefronts: component tk, tile part p ----
+        const int tk = wid / C::WPC, p = wid % C::WPC;
+        constexpr int P1 = C::WPC > 1 ? 1 : 0;
+        if (p == 0) cov16_part<D, 0>(a, img, nb, tk, nk, k0, chunk, lane);
+        else cov16_part<D, P1>(a, img, nb, tk, nk, k0, chunk, lane);
+        return;
+    }
+    // ---- staging wavefronts: 16-byte loads at d = 128, one column per thread at d = 64 ----
+    const int st = tid - 64 * C::AW;
+    if constexpr (D == 128) {
+        Cov16StageX4<D> sg(a, st, k0, nk, c0, c1);
+        cov16_staging<D>(img, sg, nb);
+    } else {
+        Cov16StageCol<D> sg(a, st, lane, k0, nk, c0, c1);
+        cov16_staging<D>(img, sg, nb);
+    }
+}
+
+// ---- M-step scatter on bf16-part MFMAs (k_gmm_cov_bf3, gmm_cov_async = 4) --------------------
+//
+// S_k = sum_i r_ik d_i d_i^T (d_i = x_i - m_k) written as E^T E with E_ik = sqrt(r_ik) d_i: one
+// operand image serves both sides of every MFMA.  E is formed and split into its three bf16 parts
+// (the bf16-part arithmetic: six exact part products per multiply-add, summed in fp32) by 4
+// staging wavefronts, ONCE per (sample, feature, component), into a feature-major LDS image (rows
+// of 32 samples, 16-byte granules of 8 samples XOR-swizzled by CovBf3::swz: conflict-free
+// ds_read_b128 fragments and ds_write_b128 stores).  The MFMA wavefronts take fragment a (32
+// features x 16 samples, one ds_read_b128 per part) as the A operand of the tiles in row a and
+// the B operand of the tiles in column a: the 10 upper 32x32 tiles of a d = 128 component (3 at
+// d = 64) split 5 / 5 over two wavefronts.  sqrt(r) adds one rounding (1 ulp) to each weight
+// against the fp32 kernels' r d: tests hold the result to their tolerances and error level.
+// Grid and output as k_gmm_cov16 (components per workgroup x row chunks, [chunk][K][d][d]).
+template <int D>
+struct CovBf3 {
+    static constexpr int RB = 32;                   // samples per block (2 k-steps)
+    static constexpr int CPW = D == 128 ? 2 : 4;    // components per workgroup
+    static constexpr int WPC = D == 128 ? COME_COV3_WPC : 1;  // MFMA wavefronts per component
+    static constexpr int AW = CPW * WPC;            // MFMA wavefronts (4)
+    static constexpr int SW = D == 128 ? COME_COV3_SW : 4;  // staging wavefronts
+    static constexpr int THREADS = 64 * (AW + SW);
+    static constexpr int NF = D / 32;               // fragments (32-feature row groups)
+    static constexpr int PLANE = D * RB * 2;        // bytes per part image (D rows x 32 bf16)
+    static constexpr int IMG = 3 * PLANE;           // per component (24 KB at d = 128)
+    static constexpr int BUF = CPW * IMG;
+    static constexpr int LDS_BYTES = 2 * BUF;       // 96 KB: one workgroup per CU
+    static constexpr int SPT = RB * D / (64 * SW);  // samples per staging thread (16 / 8)
+    static_assert(SPT % 8 == 0, "a staging thread fills whole 8-sample granules");
+    // granule swizzle: bit 0 = bit 2 of the row, bit 1 = bit 1 ^ bit 3 -- distinct over the rows
+    // of every 16-lane ds_read_b128 group (64 banks) and of every 8-lane ds_write_b128 group (32
+    // banks: 8 consecutive rows) that share a bank column
+    __host__ __device__ static constexpr int swz(int f) {
+        return ((f >> 2) & 1) | ((((f >> 1) ^ (f >> 3)) & 1) << 1);
+    }
+    __host__ __device__ static constexpr int at(int P, int f, int g) {
+        return P * PLANE + f * 64 + 16 * (g ^ swz(f));
+    }
+};
+
+// tile n of MFMA part p: (row group ta, column group tb), ta <= tb
+template <int D>
+struct CovBf3Tiles {
+    static constexpr int WPC = CovBf3<D>::WPC;
+    int cnt[4], ta[4][5], tb[4][5];
+    bool need[4][4];  // fragments a part reads
+    constexpr CovBf3Tiles() : cnt(), ta(), tb(), need() {
+        // d = 128: 10 upper tiles per component, 5 / 5 over 2 wavefronts or 3 / 3 / 2 / 2 over 4
+        const int a2[2][5] = {{0, 0, 0, 0, 3}, {1, 1, 1, 2, 2}};
+        const int b2[2][5] = {{0, 1, 2, 3, 3}, {1, 2, 3, 2, 3}};
+        const int a4[4][3] = {{0, 0, 0}, {0, 1, 3}, {1, 1, 0}, {2, 2, 0}};
+        const int b4[4][3] = {{0, 1, 2}, {3, 3, 3}, {1, 2, 0}, {2, 3, 0}};
+        const int c4[4] = {3, 3, 2, 2};
+        for (int p = 0; p < 4; ++p) {
+            if (D == 128 && WPC == 2 && p < 2) {
+                cnt[p] = 5;
+                for (int n = 0; n < 5; ++n) {
+                    ta[p][n] = a2[p][n];
+                    tb[p][n] = b2[p][n];
+                }
+            } else if (D == 128 && WPC == 4) {
+                cnt[p] = c4[p];
+                for (int n = 0; n < c4[p]; ++n) {
+                    ta[p][n] = a4[p][n];
+                    tb[p][n] = b4[p][n];
+                }
+            } else if (D == 64 && p == 0) {
+                const int a0[3] = {0, 0, 1}, b0[3] = {0, 1, 1};
+                cnt[p] = 3;
+                for (int n = 0; n < 3; ++n) {
+                    ta[p][n] = a0[n];
+                    tb[p][n] = b0[n];
+                }
+            }
+            for (int n = 0; n < cnt[p]; ++n) need[p][ta[p][n]] = need[p][tb[p][n]] = true;
+        }
+    }
+};
+
+template <int D, int P>
+__device__ __forceinline__ void covbf3_part(const CovArgs &a, const char *smb, int nb, int tk,
+                                            int nk, int k0, int64_t chunk, int lane) {
+    using C = CovBf3<D>;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr CovBf3Tiles<D> TT{};
+    constexpr int NT = TT.cnt[P];
+    const int i = lane & 31, h = lane >> 5;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[n][e] = 0.0f;
+    for (int j = 0; j < nb; ++j) {
+        __syncthreads();  // barrier j: block j staged
+        const char *im = smb + (j & 1) * C::BUF + tk * C::IMG;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            bf16x8 F[C::NF][3];
+#pragma unroll
+            for (int f = 0; f < C::NF; ++f) {
+                if (!TT.need[P][f]) continue;
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    F[f][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * f + i, 2 * st + h));
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][2], F[tb][0], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][0], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
+            }
+        }
+    }
+    if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+    float *out = a.out + (chunk * a.K + k0 + tk) * D * D;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+        const int jj = 32 * tb + i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int ii = 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+            out[(int64_t)ii * D + jj] = acc[n][r];
+            if (ta != tb) out[(int64_t)jj * D + ii] = acc[n][r];
+        }
+    }
+}
+
+// staging thread st: feature f = st % D of samples SPT sg .. SPT sg + SPT - 1 (sg = st / D,
+// uniform over a wavefront); lane l < CPW SPT of each wavefront also loads the weight r of its
+// (component l / SPT, sample l % SPT), square-rooted at stage time and broadcast by readlane
+// (a broadcast through a 128-byte LDS slot per wavefront instead -- one store, 8 ds_read_b128 --
+// was 3% slower: 5.80-5.88 vs 5.64-5.71 ms at C4)
+template <int D>
+struct CovBf3Stage {
+    using C = CovBf3<D>;
+    static constexpr int SPT = C::SPT, CPW = C::CPW;
+    static constexpr int NS = COME_COV3_NS;  // register sets: loads run NS blocks ahead
+    const CovArgs &a;
+    const int f, sg, k0, nk, lane;
+    const int64_t c0, c1;
+    float mu[CPW];
+    float xv[NS][SPT];
+    float wv[NS];
+    __device__ __forceinline__ CovBf3Stage(const CovArgs &a_, int st, int lane_, int k0_, int nk_,
+                                           int64_t c0_, int64_t c1_)
+        : a(a_), f(st % D), sg(__builtin_amdgcn_readfirstlane(st / D)), k0(k0_), nk(nk_),
+          lane(lane_), c0(c0_), c1(c1_) {
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk)
+            mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + f] : 0.0f;
+    }
+    // unconditional loads (rows clamped to the chunk, components to K - 1; zeroed when staged)
+    __device__ __forceinline__ void load(int u, int blk) {
+        const int64_t b = c0 + (int64_t)blk * C::RB + SPT * sg;
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) xv[u][q] = a.x[min(b + q, c1 - 1) * D + f];
+        const int l = lane % (CPW * SPT);
+        wv[u] = a.resp[min(b + l % SPT, c1 - 1) * a.K + min(k0 + l / SPT, a.K - 1)];
+    }
+    // the weight of lane l's (component, sample): sqrt(r), 0 past the chunk or K (so every E
+    // value of those is an exact 0 with no per-element select; x is finite, rows clamped)
+    __device__ __forceinline__ float weight(int u, int blk) const {
+        const int l = lane % (CPW * SPT);
+        const int64_t row = c0 + (int64_t)blk * C::RB + SPT * sg + l % SPT;
+        return (l / SPT < nk && row < c1) ? sqrtf(wv[u]) : 0.0f;
+    }
+    __device__ __forceinline__ void stage(float *img, int u, int blk) const {
+        char *buf = reinterpret_cast<char *>(img) + (blk % 2) * C::BUF;
+        const float w = weight(u, blk);
+#pragma unroll
+        for (int kk = 0; kk < CPW; ++kk) {
+            char *im = buf + kk * C::IMG;
+#pragma unroll
+            for (int g = 0; g < SPT / 8; ++g) {
+                uint32_t p1[4], p2[4], p3[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v[2];
+#pragma unroll
+                    for (int z = 0; z < 2; ++z) {
+                        const int q = 8 * g + 2 * e + z;
+                        const float ws =
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), kk * SPT + q));
+                        v[z] = ws * (xv[u][q] - mu[kk]);
+                    }
+                    bf16_split3(v[0], v[1], p1[e], p2[e], p3[e]);
+                }
+                const int gr = (SPT * sg) / 8 + g;  // granule of the 32-sample row
+                *reinterpret_cast<uint4 *>(im + C::at(0, f, gr)) = uint4{p1[0], p1[1], p1[2], p1[3]};
+                *reinterpret_cast<uint4 *>(im + C::at(1, f, gr)) = uint4{p2[0], p2[1], p2[2], p2[3]};
+                *reinterpret_cast<uint4 *>(im + C::at(2, f, gr)) = uint4{p3[0], p3[1], p3[2], p3[3]};
+            }
+        }
+    }
+};
+
+template <int D>
+__global__ void __launch_bounds__(CovBf3<D>::THREADS) __attribute__((amdgpu_waves_per_eu(2)))
+    k_gmm_cov_bf3(CovArgs a) {
+    using C = CovBf3<D>;
+    extern __shared__ __attribute__((aligned(16))) char smb[];
+    const int64_t chunk = blockIdx.y;
+    const int k0 = blockIdx.x * C::CPW;
+    const int nk = a.K - k0 < C::CPW ? a.K - k0 : C::CPW;
+    const int64_t c0 = chunk * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int nb = c1 > c0 ? (int)((c1 - c0 + C::RB - 1) / C::RB) : 0;
+    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wid < C::AW) {
+        // wavefronts w and w + 4 share a SIMD: with 4 parts per component, component 1's part
+        // index is shifted by 2 so that each SIMD gets 3 + 2 tiles
+        const int tk = wid / C::WPC;
+        const int p = C::WPC == 4 ? (wid % 4 + 2 * tk) % 4 : wid % C::WPC;
+        if (p == 0) covbf3_part<D, 0>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else if (p == 1) covbf3_part<D, (C::WPC > 1 ? 1 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else if (p == 2) covbf3_part<D, (C::WPC > 2 ? 2 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        else covbf3_part<D, (C::WPC > 2 ? 3 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
+        return;
+    }
+    CovBf3Stage<D> sg(a, tid - 64 * C::AW, lane, k0, nk, c0, c1);
+    cov16_staging<D>(reinterpret_cast<float *>(smb), sg, nb);
+}
+
+// Any d <= 128 on the VALU: thread owns entries tid + 256 q of the d x d output.
+__global__ void __launch_bounds__(256) k_gmm_cov_valu(CovArgs a) {
+    constexpr int MAXQ = 64;  // 128 * 128 / 256
+    __shared__ float xs[kCovRB * 129];
+    __shared__ float ws[kCovRB];
+    const int d = a.d, k = blockIdx.x, tid = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int ne = d * d;
+    float acc[MAXQ];
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) acc[q] = 0.0f;
+    for (int64_t b = c0; b < c1; b += kCovRB) {
+        __syncthreads();
+        for (int o = tid; o < kCovRB * d; o += 256) {
+            const int s = o / d, c = o % d;
+            xs[s * 129 + c] = b + s < c1 ? a.x[(b + s) * d + c] - a.means[k * d + c] : 0.0f;
+        }
+        if (tid < kCovRB) ws[tid] = b + tid < c1 ? a.resp[(b + tid) * a.K + k] : 0.0f;
+        __syncthreads();
+        const int nb = (int)((c1 - b) < kCovRB ? (c1 - b) : kCovRB);
+        for (int s = 0; s < nb; ++s) {
+            const float w = ws[s];
+            const float *row = xs + s * 129;
+#pragma unroll
+            for (int q = 0; q < MAXQ; ++q) {
+                const int e = tid + 256 * q;
+                if (e < ne) acc[q] = __builtin_fmaf(w * row[e / d], row[e % d], acc[q]);
+            }
+        }
+    }
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * ne;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+        const int e = tid + 256 * q;
+        if (e < ne) out[e] = acc[q];
+    }
+}
+
+// Scatter matrices for any d <= kMaxDim: workgroup (k, chunk, tile) accumulates the 64 x 64
+// output tile `tile` (row-major over (d/64 rounded up)^2 tiles) over the chunk's samples, staged
+// 32 at a time centred on mu_k with their weights.
+constexpr int kCovWideRB = 32;
+__global__ void __launch_bounds__(kThreads) k_gmm_cov_wide(CovArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int d = a.d, k = blockIdx.x, tid = threadIdx.x;
+    const int nt = (d + 63) / 64;
+    const int ti = blockIdx.z / nt, tj = blockIdx.z % nt;
+    float *xs = smem;                 // [kCovWideRB][d]
+    float *ws = xs + kCovWideRB * d;  // [kCovWideRB]
+    const int64_t c0 = (int64_t)blockIdx.y * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    float acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    for (int64_t b = c0; b < c1; b += kCovWideRB) {
+        __syncthreads();
+        for (int o = tid; o < kCovWideRB * d; o += kThreads) {
+            const int s = o / d, c = o % d;
+            xs[o] = b + s < c1 ? a.x[(b + s) * d + c] - a.means[k * d + c] : 0.0f;
+        }
+        if (tid < kCovWideRB) ws[tid] = b + tid < c1 ? a.resp[(b + tid) * a.K + k] : 0.0f;
+        __syncthreads();
+        const int nb = (int)((c1 - b) < kCovWideRB ? (c1 - b) : kCovWideRB);
+        for (int s = 0; s < nb; ++s) {
+            const float w = ws[s];
+            const float *row = xs + s * d;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int e = tid + 256 * q;  // (i, j) of the 64 x 64 tile
+                const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
+                if (i < d && j < d) acc[q] = __builtin_fmaf(w * row[i], row[j], acc[q]);
+            }
+        }
+    }
+    float *out = a.out + ((int64_t)blockIdx.y * a.K + k) * d * d;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int e = tid + 256 * q;
+        const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
+        if (i < d && j < d) out[(int64_t)i * d + j] = acc[q];
+    }
+}
+
+// out[i] = sum_c part[c][i] in chunk order (deterministic), i over K d^2 entries.
+__global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float *out, int64_t n,
+                                                        int chunks) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.0f;
+    for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * n + i];
+    out[i] = s;
+}
+
+}  // namespace come
+
+using namespace come;
+
+extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *resp,
+                                const float *means, int K, int chunks, float *scratch,
+                                float *scatter_out, void *stream) {
+    if (V < 0 || d < 1 || d > kMaxDim || K < 1 || chunks < 1 || chunks > 65535)
+        return set_error(COME_E_INVALID, "gmm_scatter: need V>=0, 1<=d<=%d, K>=1, "
+                                         "1<=chunks<=65535", kMaxDim);
+    if (!x || !resp || !means || !scatter_out || (chunks > 1 && !scratch))
+        return set_error(COME_E_INVALID, "null pointer");
+    int dev;
+    int rc = ensure_init(&dev);
+    if (rc) return rc;
+    const int64_t n = (int64_t)K * d * d;
+    int64_t per = (V + chunks - 1) / chunks;
+    per = (per + kCovRB - 1) / kCovRB * kCovRB;
+    if (per < kCovRB) per = kCovRB;
+    const int used = V == 0 ? 1 : (int)((V + per - 1) / per);
+    CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K};
+    const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
+    if (d > 128) {
+        const int nt = (d + 63) / 64;
+        const size_t lds = sizeof(float) * ((size_t)kCovWideRB * d + kCovWideRB);
+        static bool attr_w = false;
+        if (!attr_w) {
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_wide,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_w = true;
+        }
+        hipLaunchKernelGGL(k_gmm_cov_wide, dim3(K, used, nt * nt), dim3(kThreads), lds,
+                           (hipStream_t)stream, a);
+        rc = hip_error(hipGetLastError(), "k_gmm_cov_wide launch");
+        if (rc || used == 1) return rc;
+        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+    }
+    // gmm_cov_async: 4 (default) = k_gmm_cov_bf3 (bf16 parts), 3 = k_gmm_cov16 (fp32 16x16x4)
+    const int cv = current_opts().gmm_cov_async;
+    if (cv != 3 && cv != 4)
+        return set_error(COME_E_INVALID, "gmm_cov_async must be 3 or 4 (got %d)", cv);
+    if (mfma && cv == 4) {
+        static bool attr4 = false;
+        if (!attr4) {
+            for (void (*f)(CovArgs) : {k_gmm_cov_bf3<64>, k_gmm_cov_bf3<128>})
+                (void)hipFuncSetAttribute((const void *)f,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr4 = true;
+        }
+        const int cpw = d == 64 ? CovBf3<64>::CPW : CovBf3<128>::CPW;
+        hipLaunchKernelGGL(d == 64 ? k_gmm_cov_bf3<64> : k_gmm_cov_bf3<128>,
+                           dim3((K + cpw - 1) / cpw, used),
+                           dim3(d == 64 ? CovBf3<64>::THREADS : CovBf3<128>::THREADS),
+                           d == 64 ? CovBf3<64>::LDS_BYTES : CovBf3<128>::LDS_BYTES,
+                           (hipStream_t)stream, a);
+        rc = hip_error(hipGetLastError(), "k_gmm_cov_bf3 launch");
+        if (rc || used == 1) return rc;
+        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+    }
+    void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu : (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>);
+    const int threads = !mfma ? 256 : (d == 64 ? Cov16<64>::THREADS : Cov16<128>::THREADS);
+    const int cpw = !mfma ? 1 : (d == 64 ? Cov16<64>::CPW : Cov16<128>::CPW);
+    hipLaunchKernelGGL(kern, dim3((K + cpw - 1) / cpw, used), dim3(threads), 0,
+                       (hipStream_t)stream, a);
+    rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
+    if (rc || used == 1) return rc;
+    hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+    return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+}
