@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <immintrin.h>
+
 #include <atomic>
 #include <cmath>
 #include <thread>
@@ -79,6 +81,35 @@ HOT float dot_wave64(const float *a, const float *b, int d) {
     return lane[0];
 }
 
+// The same value with AVX2: eight 8-lane accumulators hold the 64 lanes (fma chains over d in
+// steps of 64, as above), then the butterfly's reduction tree.  The xor butterfly's lane 0 is the
+// pairwise tree over lanes 0..63 in index order (stage `off` adds the neighbouring groups of size
+// off) and float addition is commutative, so any evaluation of that tree is bit-identical:
+// hadd(A, B) forms the off=1 pairs of two accumulators, a second hadd the off=2 pairs, adding the
+// 128-bit halves the off=4 groups (one sum per accumulator), and the last three stages pair the
+// eight sums (0,1) (2,3) (4,5) (6,7), then (01,23) (45,67), then the two halves.
+// (Out of line: an always_inline target("avx2,fma") function cannot be inlined into the generic
+// template chain; the call costs nothing beside d = 128 of work.)
+__attribute__((target("avx2,fma"))) float dot_wave64_avx2(
+    const float *a, const float *b, int d) {
+    __m256 acc[8];
+    for (int j = 0; j < 8; ++j) acc[j] = _mm256_setzero_ps();
+    for (int v = 0; v < d; v += 64)
+        for (int j = 0; j < 8; ++j)
+            acc[j] = _mm256_fmadd_ps(_mm256_loadu_ps(a + v + 8 * j),
+                                     _mm256_loadu_ps(b + v + 8 * j), acc[j]);
+    const __m256 h0 = _mm256_hadd_ps(_mm256_hadd_ps(acc[0], acc[1]),
+                                     _mm256_hadd_ps(acc[2], acc[3]));
+    const __m256 h1 = _mm256_hadd_ps(_mm256_hadd_ps(acc[4], acc[5]),
+                                     _mm256_hadd_ps(acc[6], acc[7]));
+    // s0 = [S0 S1 S2 S3], s1 = [S4 S5 S6 S7]: the per-accumulator sums (stage off=4)
+    const __m128 s0 = _mm_add_ps(_mm256_castps256_ps128(h0), _mm256_extractf128_ps(h0, 1));
+    const __m128 s1 = _mm_add_ps(_mm256_castps256_ps128(h1), _mm256_extractf128_ps(h1, 1));
+    const __m128 p = _mm_hadd_ps(s0, s1);  // [S0+S1, S2+S3, S4+S5, S6+S7]   (off=8)
+    const __m128 q = _mm_hadd_ps(p, p);    // [S0..3, S4..7, ...]             (off=16)
+    return _mm_cvtss_f32(_mm_add_ss(q, _mm_movehdup_ps(q)));  //              (off=32)
+}
+
 struct Sgns {
     float *in_tab, *out_tab;  // O1: the same table (pyx:444)
     int64_t V;
@@ -90,27 +121,43 @@ struct Sgns {
     float lr, alpha;
 };
 
-// One pair (pyx:105-151 for O2, pyx:205-249 for O1: no alpha, output rows not written).
-template <bool O2>
+// Rows not yet in cache are the cost at the benchmarked sizes (a 1M x 128 table is 512 MB, a 1e8
+// table 400 MB): every row a pair touches is prefetched before the first is read.
+HOT void prefetch_row(const float *row, int d) {
+    for (int i = 0; i < d; i += 16) __builtin_prefetch(row + i, 1, 3);
+}
+
+// One pair (pyx:105-151 for O2, pyx:205-249 for O1: no alpha, output rows not written).  The
+// negative draws depend only on nr (pyx:133-134), so they are taken first -- the table reads and
+// the target rows then overlap instead of queueing behind each dot product; the update sequence
+// itself is unchanged.
+template <bool O2, bool Simd>
 HOT uint64_t pair_update(const Sgns &a, uint32_t word_index, uint32_t word2_index, uint64_t nr,
                          float *work, const float *expt) {
     float *in = a.in_tab + (int64_t)word2_index * a.d;
+    uint32_t target[kMaxNegative + 1];
+    target[0] = word_index;
+    for (int k = 1; k <= a.negative; ++k) {
+        target[k] = a.table[(nr >> 16) % a.T];
+        nr = (nr * kLcgMul + kLcgAdd) & kLcgMask;  // pyx:134
+    }
+    prefetch_row(in, a.d);
+    for (int k = 0; k <= a.negative; ++k)
+        if ((int64_t)target[k] < a.V) prefetch_row(a.out_tab + (int64_t)target[k] * a.d, a.d);
     for (int i = 0; i < a.d; ++i) work[i] = 0.0f;
     for (int k = 0; k <= a.negative; ++k) {
-        uint32_t target;
-        float label;
-        if (k == 0) {
-            target = word_index;
-            label = 1.0f;
-        } else {
-            target = a.table[(nr >> 16) % a.T];
-            nr = (nr * kLcgMul + kLcgAdd) & kLcgMask;  // pyx:134
-            if (target == word_index) continue;        // pyx:135: the draw is consumed
-            if ((int64_t)target >= a.V) continue;      // a table value outside [0, V): skipped
+        float label = 1.0f;
+        if (k > 0) {
+            if (target[k] == word_index) continue;     // pyx:135: the draw is consumed
+            if ((int64_t)target[k] >= a.V) continue;   // a table value outside [0, V): skipped
             label = 0.0f;
         }
-        float *out = a.out_tab + (int64_t)target * a.d;
-        const float f = dot_wave64(in, out, a.d);
+        float *out = a.out_tab + (int64_t)target[k] * a.d;
+        float f;
+        if constexpr (Simd)
+            f = (a.d & 63) == 0 ? dot_wave64_avx2(in, out, a.d) : dot_wave64(in, out, a.d);
+        else
+            f = dot_wave64(in, out, a.d);
         if (f <= -6.0f || f >= 6.0f) continue;         // pyx:141: skip, not clamp
         const float s = expt[(int)(((double)f + 6.0) * 83.0)];
         const float g = O2 ? ((label - s) * a.lr) * a.alpha : (label - s) * a.lr;
@@ -124,6 +171,7 @@ HOT uint64_t pair_update(const Sgns &a, uint32_t word_index, uint32_t word2_inde
 
 // train_o2 on walk p (pyx:479-508): fixed window, j ascending, j != i; entries outside [0, V) are
 // None (pyx:435-436).  Returns its pair updates.
+template <bool Simd>
 HOT int64_t walk_o2(const Sgns &a, int64_t p, float *work, const float *expt) {
     const int32_t *idx = a.items + p * (int64_t)a.L;
     const int n = a.L < kMaxSentenceLen ? a.L : kMaxSentenceLen;
@@ -136,7 +184,7 @@ HOT int64_t walk_o2(const Sgns &a, int64_t p, float *work, const float *expt) {
         const int j1 = i + a.window + 1 > n ? n : i + a.window + 1;
         for (int j = j0; j < j1; ++j) {
             if (j == i || !ok(j)) continue;
-            nr = pair_update<true>(a, (uint32_t)idx[i], (uint32_t)idx[j], nr, work, expt);
+            nr = pair_update<true, Simd>(a, (uint32_t)idx[i], (uint32_t)idx[j], nr, work, expt);
             ++pairs;
         }
     }
@@ -145,30 +193,31 @@ HOT int64_t walk_o2(const Sgns &a, int64_t p, float *work, const float *expt) {
 
 // train_o1 on edge e (pyx:425-450): (input u, positive v) then (input v, positive u), the RNG
 // state carried across both.  An edge with an endpoint outside [0, V) is skipped.
+template <bool Simd>
 HOT int64_t edge_o1(const Sgns &a, int64_t e, float *work, const float *expt) {
     const int32_t u = a.items[2 * e], v = a.items[2 * e + 1];
     if (u < 0 || v < 0 || (int64_t)u >= a.V || (int64_t)v >= a.V) return 0;
     uint64_t nr = a.seeds[e];
-    nr = pair_update<false>(a, (uint32_t)v, (uint32_t)u, nr, work, expt);
-    pair_update<false>(a, (uint32_t)u, (uint32_t)v, nr, work, expt);
+    nr = pair_update<false, Simd>(a, (uint32_t)v, (uint32_t)u, nr, work, expt);
+    pair_update<false, Simd>(a, (uint32_t)u, (uint32_t)v, nr, work, expt);
     return 2;
 }
 
-template <bool O2>
+template <bool O2, bool Simd>
 HOT int64_t run_items(const Sgns &a, int64_t lo, int64_t hi, float *work) {
     const float *expt = exp_table();
     int64_t pairs = 0;
     for (int64_t i = lo; i < hi; ++i)
-        pairs += O2 ? walk_o2(a, i, work, expt) : edge_o1(a, i, work, expt);
+        pairs += O2 ? walk_o2<Simd>(a, i, work, expt) : edge_o1<Simd>(a, i, work, expt);
     return pairs;
 }
 template <bool O2>
 COME_FMA_CLONE int64_t run_items_fma(const Sgns &a, int64_t lo, int64_t hi, float *work) {
-    return run_items<O2>(a, lo, hi, work);
+    return run_items<O2, true>(a, lo, hi, work);
 }
 template <bool O2>
 int64_t run_items_base(const Sgns &a, int64_t lo, int64_t hi, float *work) {
-    return run_items<O2>(a, lo, hi, work);
+    return run_items<O2, false>(a, lo, hi, work);
 }
 
 // `threads` workers claim jobs of kJobItems consecutive items from a shared counter and race on

@@ -9,15 +9,19 @@ Same names and argument meaning as the reference:
     init() -> int, FAST_VERSION                                         (pyx:512-549)
 
 Like the reference they mutate the embedding tables IN PLACE and draw each call's initial
-``next_random`` from the global numpy RNG (2 draws, pyx:427,477).  The tables may be CUDA
-tensors (the fast, intended path: no copies) or numpy arrays (compatibility: copied to the GPU and
-back per call).  ``py_size`` and ``py_work`` are accepted and ignored (the kernel keeps its work
-vector in registers).
+``next_random`` from the global numpy RNG (2 draws, pyx:427,477), and they are re-entrant: the
+reference's worker threads may call them concurrently.  The tables may be CUDA tensors (the
+kernels, on the current stream, no copies) or numpy arrays (libcome's host twin, in place, the GIL
+released as the reference's ``nogil`` block releases it); see "per-call drop-ins" below.
+``py_size`` and ``py_work`` are accepted and ignored (the work vector lives in registers).
 
 The batched entry points ``sgns_o2`` / ``sgns_o1`` take whole batches of walks / edges already on
 the device and are what the trainers (Context2Vec / Node2Vec) call: one launch per batch instead
 of one Python call per walk.
 """
+import ctypes
+import threading
+
 import numpy as np
 
 from . import _lib
@@ -26,6 +30,7 @@ from ._lib import (HOT_NONE, MODE_HOGWILD, MODE_SEQUENTIAL, TABLE_PACKED, check,
 
 FAST_VERSION = 0
 MAX_SENTENCE_LEN = 10000
+_SEED_LOCK = threading.Lock()
 
 
 def init():
@@ -54,16 +59,17 @@ def draw_seeds(n, out=None):
     if out is not None and (out.dtype != np.uint64 or out.shape != (n,) or
                             not out.flags["C_CONTIGUOUS"]):
         raise ValueError("out must be a contiguous uint64 array of %d seeds" % n)
-    st = np.random.get_state()
-    if st[0] != "MT19937":  # pragma: no cover (the legacy global RNG is always MT19937)
-        ab = np.random.randint(0, 2 ** 24, size=2 * n).astype(np.uint64)
-        return (ab[0::2] << np.uint64(24)) + ab[1::2]
-    state = np.empty(625, np.uint32)
-    state[:624] = st[1]
-    state[624] = st[2]
-    out = np.empty(n, np.uint64) if out is None else out
-    check(_lib.lib().come_np_draw_seeds(ptr(state), n, ptr(out)), "come_np_draw_seeds")
-    np.random.set_state((st[0], state[:624].copy(), int(state[624]), st[3], st[4]))
+    with _SEED_LOCK:  # get_state -> native draws (GIL released) -> set_state is one step
+        st = np.random.get_state()
+        if st[0] != "MT19937":  # pragma: no cover (the legacy global RNG is always MT19937)
+            ab = np.random.randint(0, 2 ** 24, size=2 * n).astype(np.uint64)
+            return (ab[0::2] << np.uint64(24)) + ab[1::2]
+        state = np.empty(625, np.uint32)
+        state[:624] = st[1]
+        state[624] = st[2]
+        out = np.empty(n, np.uint64) if out is None else out
+        check(_lib.lib().come_np_draw_seeds(ptr(state), n, ptr(out)), "come_np_draw_seeds")
+        np.random.set_state((st[0], state[:624].copy(), int(state[624]), st[3], st[4]))
     return out
 
 
@@ -241,18 +247,93 @@ def count_o2_pairs(walks_np, window):
 
 
 # ---- per-call drop-ins (reference signatures) -------------------------------------------------
+#
+# The reference's callers run train_o2 / train_o1 from `workers` Python threads at once, each call
+# releasing the GIL around its update loop (pyx:443,493; context_embeddings.py:72-98,
+# node_embeddings.py:58-83): calls must be re-entrant, and updates of one call must not undo
+# another's.  Where the tables live decides the route:
+#   * host route (every table a numpy array, the reference's own case): the call runs libcome's
+#     host twin come_cpu_sgns_o2 / _o1 in sequential mode on the caller's arrays, in place, through
+#     ctypes (which drops the GIL, as the reference's `nogil` block does).  Concurrent calls race
+#     per element exactly like the reference's threads; nothing is copied.
+#   * device route (any table a CUDA tensor): the kernels, on the caller's current stream.  numpy
+#     tables among the arguments go through cached device mirrors, and the whole
+#     upload -> launch -> writeback sequence of such a call holds _DEVICE_LOCK, so no other call's
+#     upload or writeback lands in between (a call that only has CUDA tensors takes no lock).
+# set_numpy_route("device") sends all-numpy calls down the device route as well (serialised by
+# the lock; see INTEGRATION.md for what each route costs).
+
+_DEVICE_LOCK = threading.Lock()
+_NUMPY_ROUTE = ["host"]
+
+
+def set_numpy_route(route):
+    """Where calls whose tables are all numpy arrays run: "host" (default: libcome's host twin on
+    the arrays in place) or "device" (the kernels through device mirrors, serialised)."""
+    if route not in ("host", "device"):
+        raise ValueError("route must be 'host' or 'device'")
+    prev, _NUMPY_ROUTE[0] = _NUMPY_ROUTE[0], route
+    return prev
+
+
+_PYEXT = []
+
+
+def _pyext():
+    """The host route's CPython extension (_come_pyext, csrc/come_pyext.c), bound on first use to
+    libcome's host twins; raises if it is not built (no slower Python stand-in)."""
+    if _PYEXT:
+        return _PYEXT[0]
+    with _SEED_LOCK:
+        if not _PYEXT:
+            try:
+                from . import _come_pyext as ext
+            except ImportError as e:
+                raise _lib.ComeError("_come_pyext is not built (%s): run `make -C "
+                                     "nodeembedding-to-communityembedding_amd/csrc`" % e)
+            L = _lib.lib()
+            addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+            ext.init(addr(L.come_cpu_sgns_o2), addr(L.come_cpu_sgns_o1), addr(L.come_last_error),
+                     np.random.randint)
+            _PYEXT.append(ext)
+    return _PYEXT[0]
+
+
+def _call_seed():
+    """One call's initial next_random, drawn as pyx:427/477 draws it (two global-RNG draws)."""
+    return (1 << 24) * int(np.random.randint(0, 1 << 24)) + int(np.random.randint(0, 1 << 24))
+
 
 def _rows_of(items):
     """Vocab objects (or None) -> int32 rows, -1 for None (codelens 0, pyx:483-490)."""
     return np.array([-1 if it is None else int(it.index) for it in items], np.int32)
 
 
-class _Mirrors(object):
-    """Device mirrors of the numpy arrays the per-call drop-ins are handed.
+def _host_table_arg(arr, name):
+    """A float32 [V, d] numpy embedding table for the host route, used in place."""
+    if not (isinstance(arr, np.ndarray) and arr.dtype == np.float32 and arr.ndim == 2 and
+            arr.flags.c_contiguous and arr.flags.writeable):
+        raise TypeError("%s must be a writable C-contiguous float32 [V, d] numpy array or a CUDA "
+                        "tensor" % name)
+    return arr
 
-    The reference borrows its numpy buffers with no copy (pyx:410-411,457-459).  Copying whole
-    tables per call (400 MB for a 1e8-slot negative table, V x d per embedding table) would make
-    every call O(V + T), so:
+
+def _host_neg_table(table):
+    """The negative table as contiguous uint32 (the reference reads it as np.uint32_t *,
+    pyx:421,472); an int32 array is viewed, other integer arrays are converted (a copy)."""
+    t = np.asarray(table)
+    if t.dtype == np.int32:
+        t = t.view(np.uint32)
+    if t.dtype != np.uint32 or not t.flags.c_contiguous:
+        t = np.ascontiguousarray(t, np.uint32)
+    return t
+
+
+class _Mirrors(object):
+    """Device mirrors of the numpy arrays handed to device-route calls (used under _DEVICE_LOCK).
+
+    Copying whole tables per call (400 MB for a 1e8-slot negative table, V x d per embedding
+    table) would make every call O(V + T), so:
       * a numpy embedding table gets ONE device buffer of its shape, kept across calls (keyed by
         the array's buffer address, shape and dtype) and never uploaded whole: each call uploads
         exactly the rows it can touch and downloads the same rows afterwards (rows outside the
@@ -284,7 +365,6 @@ class _Mirrors(object):
 
     def negative_table(self, arr, device):
         import torch
-        arr = np.ascontiguousarray(arr, np.uint32)
         key = (arr.__array_interface__["data"][0], arr.shape[0], str(device))
         fp = self._fingerprint(arr)
         hit = self.neg.get(key)
@@ -308,6 +388,11 @@ def _device_of(*arrays):
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def _is_tensor(a):
+    import torch
+    return isinstance(a, torch.Tensor)
+
+
 def _resolve_table(py_table, device):
     """The negative table as a CUDA int32 tensor and as host uint32 numpy (None when it is a
     tensor: then the touched rows are not computed on the host)."""
@@ -315,7 +400,7 @@ def _resolve_table(py_table, device):
     if isinstance(py_table, torch.Tensor):
         t = py_table if py_table.dtype == torch.int32 else py_table.view(torch.int32)
         return t.to(device), None
-    host = np.ascontiguousarray(py_table, np.uint32)
+    host = _host_neg_table(py_table)
     return _MIRRORS.negative_table(host, device), host
 
 
@@ -330,8 +415,9 @@ def _draw_rows(seed, count, host_table):
 
 
 class _Borrowed(object):
-    """One reference-style table argument for one call: a CUDA tensor is used as is; a numpy
-    array goes through its device mirror, `rows` up before the launch and down after it."""
+    """One reference-style table argument for one device-route call: a CUDA tensor is used as
+    is; a numpy array goes through its device mirror, `rows` up before the launch and down after
+    it (the caller holds _DEVICE_LOCK)."""
 
     def __init__(self, arr, device, rows):
         import torch
@@ -339,10 +425,7 @@ class _Borrowed(object):
         if isinstance(arr, torch.Tensor):
             self.dev, self.rows = arr, None
             return
-        if not (isinstance(arr, np.ndarray) and arr.dtype == np.float32 and arr.ndim == 2 and
-                arr.flags.c_contiguous):
-            raise TypeError("embedding tables must be C-contiguous float32 [V, d] numpy arrays "
-                            "or CUDA tensors")
+        _host_table_arg(arr, "embedding table")
         self.dev = _MIRRORS.table(arr, device)
         r = np.unique(rows)
         self.rows = r[(r >= 0) & (r < arr.shape[0])]
@@ -356,60 +439,131 @@ class _Borrowed(object):
             self.arr[self.rows] = self.dev.index_select(0, self.ridx).cpu().numpy()
 
 
+def _host_o2(node, ctx, rows, nr, lr, negative, window, table, alpha):
+    _host_table_arg(node, "py_node_embedding")
+    _host_table_arg(ctx, "py_context_embedding")
+    if node.shape != ctx.shape:
+        raise ValueError("node and context embeddings must have the same shape")
+    tab = _host_neg_table(table)
+    seed = ctypes.c_uint64(nr)
+    check(_lib.lib().come_cpu_sgns_o2(node.ctypes.data, ctx.ctypes.data, node.shape[0],
+                                      node.shape[1], rows.ctypes.data, 1, rows.shape[0],
+                                      ctypes.byref(seed), int(window), int(negative),
+                                      tab.ctypes.data, tab.shape[0], float(lr), float(alpha),
+                                      MODE_SEQUENTIAL, 1, None), "come_cpu_sgns_o2")
+
+
+def _device_o2(node_in, ctx_in, rows, nr, lr, negative, window, table_in, alpha):
+    import torch
+    device = _device_of(node_in, ctx_in, table_in)
+    table, host_table = _resolve_table(table_in, device)
+    walk_rows = rows[rows >= 0].astype(np.int64)
+    ctx_rows = walk_rows
+    if not _is_tensor(ctx_in):  # positives are walk rows; negatives come from this call's draws
+        if host_table is None:
+            host_table = table.cpu().numpy().view(np.uint32)
+        pairs = count_o2_pairs(rows.reshape(1, -1), window)
+        ctx_rows = np.concatenate([walk_rows, _draw_rows(nr, pairs * int(negative),
+                                                         host_table)])
+    node = _Borrowed(node_in, device, walk_rows)
+    ctx = _Borrowed(ctx_in, device, ctx_rows)
+    walks = torch.from_numpy(rows.reshape(1, -1)).to(device)
+    seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(device)
+    sgns_o2(node.dev, ctx.dev, walks, seeds, window, negative, table, lr, alpha, MODE_SEQUENTIAL)
+    node.writeback()
+    ctx.writeback()
+
+
+def _route(*args):
+    """"host", "device" (CUDA tensors only: no lock needed) or "locked" (device route with numpy
+    arguments mirrored: under _DEVICE_LOCK)."""
+    tensors = [_is_tensor(a) for a in args]
+    if all(tensors):
+        return "device"
+    if any(tensors) or _NUMPY_ROUTE[0] == "device":
+        return "locked"
+    return "host"
+
+
 def train_o2(py_node_embedding, py_context_embedding, py_path, py_lr, py_negative, py_window,
              py_table, py_alpha=1.0, py_size=None, py_work=None):
-    """One walk (pyx:454-509).  Returns the number of non-None entries.  Tables may be CUDA
-    tensors (used in place) or numpy arrays (mutated in place through cached device mirrors,
-    moving only the rows this walk can touch; see _Mirrors)."""
-    import torch
-    nr = int(draw_seeds(1)[0])  # pyx:477: two draws from the global numpy RNG, per call
-    items = list(py_path)[:MAX_SENTENCE_LEN]
-    rows = _rows_of(items)
+    """One walk (pyx:454-509).  Returns the number of non-None entries.  numpy tables are updated
+    in place by libcome's host twin (re-entrant: the reference's worker threads may call it
+    concurrently); CUDA tensors by the kernel on the current stream (see the routes above)."""
+    if (type(py_node_embedding) is np.ndarray and type(py_context_embedding) is np.ndarray and
+            type(py_table) is np.ndarray and _NUMPY_ROUTE[0] == "host"):
+        try:  # the reference's own case, in C: seeds, path rows, the twin with the GIL released
+            return _pyext().train_o2(py_node_embedding, py_context_embedding, py_path, py_lr,
+                                     py_negative, py_window, py_table, py_alpha)
+        except TypeError:  # raised before the RNG draw: e.g. a non-uint32 table, converted below
+            pass
+    nr = _call_seed()  # pyx:477: two draws from the global numpy RNG, per call
+    rows = _rows_of(py_path[:MAX_SENTENCE_LEN] if isinstance(py_path, (list, tuple))
+                    else list(py_path)[:MAX_SENTENCE_LEN])
     result = int((rows >= 0).sum())
     if not rows.size:
         return result
-    device = _device_of(py_node_embedding, py_context_embedding, py_table)
-    table, host_table = _resolve_table(py_table, device)
-    walk_rows = rows[rows >= 0].astype(np.int64)
-    ctx_rows = walk_rows
-    numpy_ctx = not isinstance(py_context_embedding, torch.Tensor)
-    if numpy_ctx:  # positives are walk rows; negatives come from this call's draws
+    args = (py_node_embedding, py_context_embedding, rows, nr, py_lr, py_negative, py_window,
+            py_table, py_alpha)
+    route = _route(py_node_embedding, py_context_embedding, py_table)
+    if route == "host":
+        _host_o2(*args)
+    elif route == "device":
+        _device_o2(*args)
+    else:
+        with _DEVICE_LOCK:
+            _device_o2(*args)
+    return result
+
+
+def _host_o1(node, rows, nr, lr, negative, table):
+    _host_table_arg(node, "py_node_embedding")
+    tab = _host_neg_table(table)
+    seed = ctypes.c_uint64(nr)
+    check(_lib.lib().come_cpu_sgns_o1(node.ctypes.data, node.shape[0], node.shape[1],
+                                      rows.ctypes.data, 1, ctypes.byref(seed), int(negative),
+                                      tab.ctypes.data, tab.shape[0], float(lr), MODE_SEQUENTIAL,
+                                      1, None), "come_cpu_sgns_o1")
+
+
+def _device_o1(node_in, rows, nr, lr, negative, table_in):
+    import torch
+    device = _device_of(node_in, table_in)
+    table, host_table = _resolve_table(table_in, device)
+    touched = rows[rows >= 0].astype(np.int64)
+    if not _is_tensor(node_in):
         if host_table is None:
             host_table = table.cpu().numpy().view(np.uint32)
-        pairs = count_o2_pairs(rows.reshape(1, -1), py_window)
-        ctx_rows = np.concatenate([walk_rows, _draw_rows(nr, pairs * int(py_negative),
-                                                         host_table)])
-    node = _Borrowed(py_node_embedding, device, walk_rows)
-    ctx = _Borrowed(py_context_embedding, device, ctx_rows)
-    walks = torch.from_numpy(rows.reshape(1, -1)).to(device)
+        touched = np.concatenate([touched, _draw_rows(nr, 2 * int(negative), host_table)])
+    node = _Borrowed(node_in, device, touched)
+    edges = torch.from_numpy(rows.reshape(1, 2)).to(device)
     seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(device)
-    sgns_o2(node.dev, ctx.dev, walks, seeds, py_window, py_negative, table, py_lr, py_alpha,
-            MODE_SEQUENTIAL)
+    sgns_o1(node.dev, edges, seeds, negative, table, lr, MODE_SEQUENTIAL)
     node.writeback()
-    ctx.writeback()
-    return result
 
 
 def train_o1(py_node_embedding, py_edge, py_lr, py_negative, py_table, py_size=None, py_work=None):
     """One edge (pyx:407-450): pairs (edge[0] -> edge[1]) then (edge[1] -> edge[0]).  Returns the
-    number of non-None endpoints.  numpy tables: only the edge's rows and its 2n negative rows
-    cross to and from the device."""
-    import torch
-    nr = int(draw_seeds(1)[0])  # pyx:427
+    number of non-None endpoints.  Routes as train_o2 (numpy: the host twin in place; CUDA
+    tensors: the kernel)."""
+    if (type(py_node_embedding) is np.ndarray and type(py_table) is np.ndarray and
+            _NUMPY_ROUTE[0] == "host"):
+        try:
+            return _pyext().train_o1(py_node_embedding, py_edge, py_lr, py_negative, py_table)
+        except TypeError:
+            pass
+    nr = _call_seed()  # pyx:427
     rows = _rows_of(list(py_edge)[:2])
     result = int((rows >= 0).sum())
     if rows.size != 2:
         return result
-    device = _device_of(py_node_embedding, py_table)
-    table, host_table = _resolve_table(py_table, device)
-    touched = rows[rows >= 0].astype(np.int64)
-    if not isinstance(py_node_embedding, torch.Tensor):
-        if host_table is None:
-            host_table = table.cpu().numpy().view(np.uint32)
-        touched = np.concatenate([touched, _draw_rows(nr, 2 * int(py_negative), host_table)])
-    node = _Borrowed(py_node_embedding, device, touched)
-    edges = torch.from_numpy(rows.reshape(1, 2)).to(device)
-    seeds = torch.from_numpy(np.array([nr], np.uint64).view(np.int64)).to(device)
-    sgns_o1(node.dev, edges, seeds, py_negative, table, py_lr, MODE_SEQUENTIAL)
-    node.writeback()
+    args = (py_node_embedding, rows, nr, py_lr, py_negative, py_table)
+    route = _route(py_node_embedding, py_table)
+    if route == "host":
+        _host_o1(*args)
+    elif route == "device":
+        _device_o1(*args)
+    else:
+        with _DEVICE_LOCK:
+            _device_o1(*args)
     return result

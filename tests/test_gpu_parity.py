@@ -255,11 +255,21 @@ def test_o2_dropin_per_walk_numpy_and_tensor():
     np.testing.assert_array_equal(tnode.cpu().numpy(), node)
 
 
-def test_dropin_per_call_cost_independent_of_table_sizes():
-    """The per-call drop-ins move only the rows a walk / edge can touch (numpy tables through
-    cached device mirrors, the negative table uploaded once): per-call time must not grow with
-    T (1e4 -> 2e7 slots) or V (2e3 -> 2e6 rows), and the numpy results must equal the CUDA-tensor
-    path's bit for bit."""
+@pytest.mark.parametrize("route", ["host", "device"])
+def test_dropin_per_call_cost_independent_of_table_sizes(route):
+    """The per-call drop-ins touch only the rows a walk / edge can touch: numpy tables on the host
+    route (libcome's host twin in place) or forced down the device route (cached device mirrors,
+    the negative table uploaded once).  Per-call time must not grow with T (1e4 -> 2e7 slots) or
+    V (2e3 -> 2e6 rows), and the numpy results must equal the CUDA-tensor path's bit for bit."""
+    import time
+    prev = tsi.set_numpy_route(route)
+    try:
+        _per_call_cost(route)
+    finally:
+        tsi.set_numpy_route(prev)
+
+
+def _per_call_cost(route):
     import time
 
     class V_:
@@ -291,7 +301,8 @@ def test_dropin_per_call_cost_independent_of_table_sizes():
         np.testing.assert_array_equal(tnode.cpu().numpy(), node)
         np.testing.assert_array_equal(tctx.cpu().numpy(), ctx)
     small, big = times[(2000, 10_000)], times[(2_000_000, 20_000_000)]
-    print("per call: small tables %.3f ms, large tables %.3f ms" % (small * 1e3, big * 1e3))
+    print("per call (%s route): small tables %.3f ms, large tables %.3f ms" % (
+        route, small * 1e3, big * 1e3))
     assert big < 2.0 * small + 2e-3, times
 
 
