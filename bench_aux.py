@@ -236,11 +236,16 @@ def c4(args):
         orc.community_train(xs, pi[:S].cpu().numpy(), mu.cpu().numpy(), inv.cpu().numpy(),
                             0.01, 0.1, 1)
         cel = time.time() - t0
+        blas = blas_threads()
         cpu = {"value": 2.0 * S * K * d * d / cel / 1e12, "unit": "TFLOP/s", "cores": 1,
-               "kind": "port",
+               "kind": "port", "blas_threads": blas,
                "sample": "Community2Vec.train's numpy loop (community_embeddings.py:61-78, "
                          "restated op for op in oracle/oracle.py) on %d of the %d rows: "
-                         "%.2fs -> %.0f s per full pass" % (S, V, cel, cel * V / S)}
+                         "%.2fs -> %.0f s per full pass.  cores 1: the loop's time is numpy's "
+                         "elementwise pi * inv_cov products and its stacked [150 x d x d] @ "
+                         "[150 x d x 1] matmul, which numpy runs on the calling thread whatever "
+                         "the BLAS pool (%s BLAS threads were available); the reference adds no "
+                         "threading of its own" % (S, V, cel, cel * V / S, blas)}
         from sklearn.mixture import GaussianMixture as SkGMM
         S2 = 20000
         Xs = x0[:S2].cpu().numpy()
@@ -258,7 +263,9 @@ def c4(args):
             sel = time.time() - t0
         cpu["gmm_em_iteration_sample"] = (
             "sklearn GaussianMixture E+M step (community_embeddings.py:27's estimator) on %d "
-            "rows: %.2fs -> %.1f s per full-size iteration" % (S2, sel, sel * V / S2))
+            "rows: %.2fs -> %.1f s per full-size iteration, its GEMMs on %s BLAS threads" % (
+                S2, sel, sel * V / S2, blas))
+        cpu["gmm_em_iteration_cores"] = blas
     dist_cfg = {}
     if world > 1:
         dist_cfg = {"community_kernel_only_ms": tk * 1e3,
@@ -356,6 +363,17 @@ def walks(args):
                      "algorithmic_frac_of_hbm": bps * steps_per_launch / avg / 1e9 / HBM_PEAK_GBS,
                      "avg_kernel_ms": avg * 1e3},
         "cpu_baseline": cpu}))
+
+
+def blas_threads():
+    """Threads of the BLAS pool numpy / scipy / sklearn run on in this process (threadpoolctl),
+    None if it cannot tell."""
+    try:
+        from threadpoolctl import threadpool_info
+        n = [i.get("num_threads") for i in threadpool_info() if i.get("user_api") == "blas"]
+        return max(n) if n else None
+    except Exception:
+        return None
 
 
 def main():

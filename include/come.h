@@ -33,15 +33,18 @@
 extern "C" {
 #endif
 
-/* ABI 3 (this header): the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B
- * kernels) was removed, "community_async" accepts 2 / 3, "gmm_cov_async" 3 / 4 and "gmm_resp16"
- * 2 / 3 (other values: COME_E_INVALID at the call; round 5 made the bf16-part kernels the
- * defaults and removed the 32x32 fp32 fallbacks 1 / 1 / 0); come_source_sha256 was added.
+/* ABI 4 (this header): the launch options "community_async" accept 2 / 3, "gmm_cov_async" 3 / 4
+ * and "gmm_resp16" 2 / 3 only -- the 32x32 fp32 fallbacks that ABI 3's values 1 / 1 / 0 selected
+ * were removed (COME_E_INVALID at the call now) -- and their defaults became the bf16-part MFMA
+ * kernels (3 / 4 / 3: fp32 operands as three bf16 parts, fp32-level error).
+ * ABI 3: the launch option "gmm_resp_db" (the double-buffered 32x32 E-step A/B kernels) was
+ * removed, "community_async" accepts 1 / 2 / 3, "gmm_cov_async" 1 / 3 / 4 and "gmm_resp16"
+ * 0 / 2 / 3 (other values: COME_E_INVALID at the call); come_source_sha256 was added.
  * ABI 2: come_*_ex hot_rows == NULL in COME_MODE_HOGWILD now means "derive the
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
  * options "o2_plain_writeback" and "o2_pair_atomics" (ABI 1, ring-kernel Hogwild) were removed and
  * come_set_option rejects them; o2_kernel = 2 with COME_MODE_HOGWILD returns COME_E_INVALID. */
-#define COME_ABI_VERSION 3
+#define COME_ABI_VERSION 4
 
 enum {
     COME_OK = 0,

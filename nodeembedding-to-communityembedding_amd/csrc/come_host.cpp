@@ -137,7 +137,8 @@ static come_launch_opts g_opts = [] {
     // needs sparse updates: with every wavefront holding ~17 rows (O2: the 2w+1 window, the
     // positive, the pair's negatives; O1 12), a vocabulary smaller than ~16 rows per wavefront
     // in flight has most rows held by several wavefronts at once and the embeddings stop
-    // converging -- measured on a 2,000-node planted partition (scripts/diag_hogwild.py):
+    // converging -- measured on a 2,000-node planted partition (round 1; the numbers are in
+    // profiles/r01_hogwild_concurrency_nmi.txt, the one-off script is gone):
     // community NMI 0.75 with 6,000 waves in flight, 0.97-0.98 with <= V/16 (= the sequential
     // run's 0.97); at 100,000 nodes the cap is inactive (V/16 > occupancy) and NMI 0.99 either way.
     o.rows_per_wave = 16;

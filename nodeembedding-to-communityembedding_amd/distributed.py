@@ -201,26 +201,62 @@ class _LocalWork(object):
 
 
 REAL_CHANGE_REL = 2.0 ** -20  # 8 ulps of fp32: above any rounding an exchange leaves behind
+REAL_CHANGE_FRAC = 8          # a real change moves at least 1/8 of the row's elements that far
 
 
 def _real_change(delta, base):
-    """Per row: does some element of ``delta`` exceed 8 ulps of the same element of ``base``?  A
-    real SGD update of a row moves at least one element by far more than that (even with a
-    decayed learning rate on a large-norm row, its small elements move by many of their own
-    ulps); the residue an overlapped exchange leaves on rows nobody changed is a few ulps."""
+    """Per row: do at least max(1, d / REAL_CHANGE_FRAC) elements of ``delta`` exceed 8 ulps of
+    the same element of ``base``?  A real SGD update of a row is a dense vector (g times another
+    row, pyx:146-147): even with a decayed learning rate on a large-norm row it moves nearly every
+    element by many of its own ulps.  The residue an overlapped exchange leaves on a row nobody
+    changed is a few ulps of the exchange's operands -- above 8 ulps of the element itself only
+    where the element lost most of its magnitude in that exchange (it crossed zero), which a few
+    elements of a row do, not an eighth of them (a per-element "any" let such a
+    crossing mark a rounding-only row as real)."""
     import torch
     if isinstance(delta, np.ndarray):
         v = np.abs(delta.reshape(delta.shape[0], -1).astype(np.float32))
         b = np.abs(base.reshape(base.shape[0], -1).astype(np.float32))
-        return (v > b * np.float32(REAL_CHANGE_REL)).any(axis=1)
+        need = max(1, v.shape[1] // REAL_CHANGE_FRAC)
+        return (v > b * np.float32(REAL_CHANGE_REL)).sum(axis=1) >= need
     v = delta.reshape(delta.shape[0], -1)
     b = base.reshape(base.shape[0], -1)
+    need = max(1, v.shape[1] // REAL_CHANGE_FRAC)
     out = torch.zeros(v.shape[0], dtype=torch.bool, device=v.device)
     step = max(1, (1 << 24) // max(1, v.shape[1]))  # row blocks: temporaries of <= 64 MB
     for lo in range(0, v.shape[0], step):
         hi = min(lo + step, v.shape[0])
-        out[lo:hi] = (v[lo:hi].abs() > b[lo:hi].abs() * REAL_CHANGE_REL).any(dim=1)
+        out[lo:hi] = (v[lo:hi].abs() > b[lo:hi].abs() * REAL_CHANGE_REL).sum(dim=1) >= need
     return out
+
+
+def _checksums(tables):
+    """Per table: the int64 sum of its 32-bit words, in blocks of 16M elements (no table-sized
+    temporary).  Two replicas with equal sums are taken to be equal."""
+    import torch
+    out = []
+    for t in tables:
+        w = t.reshape(-1).view(torch.int32)
+        acc = torch.zeros((), dtype=torch.int64, device=t.device)
+        for lo in range(0, w.numel(), 1 << 24):
+            acc += w[lo:lo + (1 << 24)].sum(dtype=torch.int64)
+        out.append(acc)
+    return torch.stack(out) if out else torch.zeros(0, dtype=torch.int64)
+
+
+def _replicas_agree(comm, tables):
+    """True when every rank's tables have the same checksums (_checksums): one all-reduce of 2 x
+    len(tables) int64 (MAX of s and of -s, i.e. max and min), instead of broadcasting the tables.
+    A one-process simulation (LocalReplicas) cannot run a blocking collective: it reports False,
+    so its callers broadcast as before."""
+    if isinstance(comm, _LocalComm):
+        return False
+    import torch
+    c = _checksums(tables)
+    both = torch.cat([c, -c])
+    comm.all_reduce(both, op="max")
+    n = c.numel()
+    return bool(torch.equal(both[:n], -both[n:]))
 
 
 def _fused(t):
@@ -293,14 +329,17 @@ class DeltaAllReduce(object):
         """Make the current tables the sync base (W_sync = W), after taking rank 0's tables (the
         replicas must agree).  Call when the tables changed outside the exchange (e.g. another
         trainer's distributed step), so that change is not counted once per rank as a delta.
-        ``broadcast=None``: broadcast only when the replicas may differ -- not after a blocking
-        sync() (which leaves them bit-identical; a trainer's train() ends with one), provided
-        whatever changed the tables since did so identically on every rank, as every distributed
-        step of this package does.  That skips a whole-table broadcast per train() call (2 GB of
-        xGMI traffic per call at C3, 41 GB at C5's shard).  True / False force it."""
+        ``broadcast=None``: broadcast when the replicas may differ.  After a blocking sync() (which
+        leaves them bit-identical; a trainer's train() ends with one) the ranks first compare
+        table checksums (_replicas_agree: one all-reduce of a few int64) and broadcast only if
+        they differ -- a non-distributed step that ran differently per rank, or an in-place edit
+        on one rank, is repaired as before, while the common case skips a whole-table
+        broadcast per train() call (2 GB of xGMI traffic per call at C3, 41 GB at C5's shard).
+        True / False force it."""
         self.finish()
         if self.active:
-            if broadcast or (broadcast is None and not self.synced):
+            if broadcast or (broadcast is None and not (self.synced and
+                                                        _replicas_agree(self.comm, self.tables))):
                 self._broadcast()
             for t, s in zip(self.tables, self.snap):
                 s.copy_(t)
@@ -466,7 +505,8 @@ class SparseDeltaAllReduce(object):
         replicas identical)."""
         self.finish()
         if self.active:
-            if broadcast or (broadcast is None and not self.synced):
+            if broadcast or (broadcast is None and not (self.synced and
+                                                        _replicas_agree(self.comm, self.tables))):
                 self._broadcast()
             for t, s in zip(self.tables, self.snap):
                 s.copy_(t)

@@ -324,3 +324,74 @@ def test_pick_real_change_on_a_large_norm_row():
     np.testing.assert_array_equal(tabs[0][1].numpy(), locs[1][1])   # rank 1's delta won
     np.testing.assert_allclose(tabs[0].numpy(), reference_pick(w_sync, locs, 0), rtol=0, atol=0)
     assert torch.equal(tabs[1], tabs[0])
+
+
+def _worker_reset(rank, world, port, out_dir):
+    """reset(broadcast=None) after a blocking sync() compares table checksums across
+    ranks and broadcasts rank 0's tables only if they differ."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from come_amd.distributed import SparseDeltaAllReduce
+    for cls in (DeltaAllReduce, SparseDeltaAllReduce):
+        rng = np.random.RandomState(0)
+        tables = [torch.from_numpy(rng.randn(37, 8).astype(np.float32)) for _ in range(2)]
+        ex = cls(tables)
+        calls = [0]
+        orig = ex._broadcast
+
+        def counted():
+            calls[0] += 1
+            orig()
+        ex._broadcast = counted
+        tables[0][rank] += 1.0       # each rank trains a little, then a blocking sync
+        ex.sync()
+        ex.reset()                   # replicas identical: checksums agree, no broadcast
+        assert calls[0] == 0
+        if rank == 1:                # an in-place edit on one rank between two train() calls
+            tables[1][5] *= 3.0
+        ex.reset()
+        assert calls[0] == 1, calls  # every rank saw the mismatch and took rank 0's tables
+        got = [None] * world
+        dist.all_gather_object(got, [t.numpy().tobytes() for t in tables])
+        assert got[0] == got[1]
+    dist.destroy_process_group()
+
+
+def test_reset_repairs_replicas_that_drifted_after_a_sync(tmp_path):
+    mp.spawn(_worker_reset, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def test_real_change_ignores_a_zero_crossing_rounding_residue():
+    """an element that crossed zero in an exchange is tiny in W_sync while the residue
+    the exchange left on it is an ulp of its old, large operands -- many ulps of the element
+    itself.  A row whose only change is such a residue is not a real change (it must not win the
+    row in pick over a rank that trained it); a dense small update still is."""
+    from come_amd.distributed import LocalReplicas, reference_pick, _real_change
+    W, V, d = 2, 3, 64
+    rng = np.random.RandomState(4)
+    base = torch.from_numpy(rng.uniform(0.5, 1.5, (V, d)).astype(np.float32))
+    base[1, 3] = 3e-8                          # crossed zero: tiny now
+    tabs = [base.clone() for _ in range(W)]
+    g = LocalReplicas(W)
+    exs = [DeltaAllReduce([tabs[r]], comm=g.comm(r), combine="pick") for r in range(W)]
+    tabs[0][1, 3] += 6e-8                      # rank 0 (the star): an ulp of 1.0 left on it
+    tabs[1][1] += torch.from_numpy(rng.uniform(-1e-4, 1e-4, d).astype(np.float32))  # trained
+    w_sync = base.numpy().copy()
+    d0 = (tabs[0] - base).numpy()
+    assert (np.abs(d0) > np.abs(w_sync) * 2.0 ** -20).any(axis=1)[1]  # the old rule: "real"
+    assert not _real_change(d0, w_sync)[1]
+    assert not bool(_real_change(tabs[0] - base, base)[1])             # torch path agrees
+    assert _real_change((tabs[1] - base).numpy(), w_sync)[1]
+    locs = [t.numpy().copy() for t in tabs]
+    assert not np.array_equal(locs[0][1], locs[1][1])
+    for e in exs:
+        e.prepare()
+    for e in exs:
+        e.start()
+    for e in exs:
+        e.finish()
+        e.settle()
+    np.testing.assert_array_equal(tabs[0][1].numpy(), locs[1][1])      # rank 1's update won
+    np.testing.assert_allclose(tabs[0].numpy(), reference_pick(w_sync, locs, 0), rtol=0, atol=0)
+    assert torch.equal(tabs[1], tabs[0])

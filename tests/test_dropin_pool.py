@@ -135,24 +135,30 @@ def test_o2_dropin_under_reference_worker_pool(o2_shape, route):
 
 @pytest.fixture(scope="module")
 def o1_shape():
-    """C2's generator at 20 blocks x 1,000 nodes (p_in 0.016: ~160k edges), d=128, n=5, lr 0.1;
-    2% of the edges held out; the kept edges in G.edges() order (node_embeddings.py:39)."""
+    return o1_inputs()
+
+
+def o1_inputs():
+    """C2's generator at 10 blocks x 500 nodes (p_in 0.03: ~37k edges), d=128, n=5, lr 0.1, the
+    reference's init (model.py:86: uniform(-1, 1)); 5% of the edges held out, the rest shuffled."""
     from come_amd.graph import sbm
-    g = sbm(20, 1000, 0.016, 4.04e-5, seed=3)
+    g = sbm(10, 500, 0.03, 4.04e-5, seed=3)
     rng = np.random.RandomState(31)
     e = g.edges[rng.permutation(len(g.edges))].astype(np.int32)
-    k = len(e) // 50
-    train = e[k:]
-    train = train[np.lexsort((train[:, 1], train[:, 0]))]
+    k = len(e) // 20
     table = orc.make_table(g.degree.astype(np.float64), 10_000_000)
     node0 = rng.uniform(-1, 1, (g.V, 128)).astype(np.float32)
-    seeds = rng.randint(0, 2 ** 48, len(train), dtype=np.int64).astype(np.uint64)
-    return g, table, train, e[:k], node0, seeds
+    return g, table, e[k:], e[:k], node0
 
 
 @pytest.mark.parametrize("route", ROUTES)
 def test_o1_dropin_under_reference_worker_pool(o1_shape, route):
-    g, table, train, held, node0, seeds = o1_shape
+    """Tier C for O1 against the sequential oracle fed the pool's own seed stream (the global
+    RNG from the same seed, in call order).  O1 from the reference's init at lr 0.1 is chaotic at
+    this size: two sequential runs that differ only in their seed stream land up to a few percent
+    apart on the reference's loss (node_embeddings.py:26-31), so the bar is 1% or twice that
+    measured seed spread, whichever is larger, and the spread is printed beside the result."""
+    g, table, train, held, node0 = o1_shape
     n, lr = 5, 0.1
     rng = np.random.RandomState(32)
     neg = table[rng.randint(0, len(table), (len(held), n))].astype(np.int64)
@@ -166,8 +172,6 @@ def test_o1_dropin_under_reference_worker_pool(o1_shape, route):
     vocab = [Vocab(i) for i in range(g.V)]
     items = [[vocab[u], vocab[v]] for u, v in train]
     (node, tab), host = _tables(route, node0.copy(), table)
-    if route == "locked":  # ~1 ms per serialised call: a quarter of the edges
-        items = items[::4]
     prev = tsi.set_numpy_route("device" if route == "locked" else "host")
     try:
         np.random.seed(6)
@@ -178,15 +182,58 @@ def test_o1_dropin_under_reference_worker_pool(o1_shape, route):
     x = host(node)
     assert np.isfinite(x).all()
     l_pool = losses(x)
-    seq = node0.copy()
-    sub = train if route != "locked" else train[::4].copy()
-    orc.sgns_o1_hogwild(seq, sub, seeds[:len(sub)].copy(), n, table, lr, threads=1)
-    l_seq = losses(seq)
-    print("O1 pool (%s, %d workers): init %.1f / %.5f  seq %.1f / %.5f  pool %.1f / %.5f" % (
-        (route, WORKERS) + l0 + l_seq + l_pool))
+    seqs = []
+    for seed in (6, 60):
+        np.random.seed(seed)
+        sd = tsi.draw_seeds(len(train))
+        s = node0.copy()
+        orc.sgns_o1_hogwild(s, train, sd, n, table, lr, threads=1)
+        seqs.append(losses(s))
+    l_seq = seqs[0]
+    spread = [abs(a - b) / abs(b) for a, b in zip(seqs[1], seqs[0])]
+    print("O1 pool (%s, %d workers): init %.1f / %.5f  seq %.1f / %.5f  pool %.1f / %.5f  "
+          "seed spread %.4f / %.4f" % ((route, WORKERS) + l0 + l_seq + l_pool + tuple(spread)))
     assert l_seq[1] < l0[1] - 0.05
-    for a, b in zip(l_pool, l_seq):
-        assert abs(a - b) / abs(b) < 0.01, (l_pool, l_seq)  # SURVEY.md §8c tier C
+    for a, b, sp in zip(l_pool, l_seq, spread):
+        assert abs(a - b) / abs(b) < max(0.01, 2 * sp), (l_pool, l_seq, spread)  # tier C
+
+
+@pytest.mark.gpu
+def test_locked_route_pool_equals_its_serial_replay(o2_shape):
+    """No lost updates on the device route with numpy tables: under the worker pool, the route's
+    lock makes every call's upload -> launch -> writeback atomic, so the pool's result must equal
+    -- bit for bit -- the host twin run sequentially over the calls in the order they took the
+    lock, with the seeds they drew (the sequential kernel and the twin agree bit for bit).  Hub
+    rows appear in nearly every call, so a single interleaved upload or writeback would show."""
+    import threading as th
+    from come_amd import cpu
+    g, table, train, held, node0, seeds = o2_shape
+    w, n, lr = 5, 5, 0.1
+    train = train[:1500]
+    vocab = [Vocab(i) for i in range(g.V)]
+    paths = [[vocab[x] if x >= 0 else None for x in row] for row in train]
+    log = []
+    orig = tsi._device_o2
+
+    def logged(node, ctx, rows, nr, *rest):
+        log.append((rows.copy(), nr))  # runs under the route's lock: execution order
+        return orig(node, ctx, rows, nr, *rest)
+    node, ctx = node0.copy(), np.zeros_like(node0)
+    prev = tsi.set_numpy_route("device")
+    tsi._device_o2 = logged
+    try:
+        np.random.seed(5)
+        run_pool(paths, lambda p: tsi.train_o2(node, ctx, p, lr, n, w, table))
+    finally:
+        tsi._device_o2 = orig
+        tsi.set_numpy_route(prev)
+    assert len(log) == len(train) and isinstance(tsi._DEVICE_LOCK, type(th.Lock()))
+    rn, rc = node0.copy(), np.zeros_like(node0)
+    walks = np.stack([r for r, _ in log]).astype(np.int32)
+    sd = np.array([s for _, s in log], np.uint64)
+    cpu.sgns_o2(rn, rc, walks, sd, w, n, table, lr, 1.0, cpu.MODE_SEQUENTIAL, threads=1)
+    np.testing.assert_array_equal(node, rn)
+    np.testing.assert_array_equal(ctx, rc)
 
 
 def test_host_route_matches_sequential_twin_bit_for_bit():

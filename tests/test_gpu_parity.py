@@ -261,7 +261,6 @@ def test_dropin_per_call_cost_independent_of_table_sizes(route):
     route (libcome's host twin in place) or forced down the device route (cached device mirrors,
     the negative table uploaded once).  Per-call time must not grow with T (1e4 -> 2e7 slots) or
     V (2e3 -> 2e6 rows), and the numpy results must equal the CUDA-tensor path's bit for bit."""
-    import time
     prev = tsi.set_numpy_route(route)
     try:
         _per_call_cost(route)
