@@ -52,6 +52,29 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #ifndef COME_COV3_WPC
 #define COME_COV3_WPC 2
 #endif
+// k_gmm_cov_fb3: staging register sets, and sched_group_barrier interleaving (A/B hooks)
+#ifndef COME_COVF_NS
+#define COME_COVF_NS 3
+#endif
+#ifndef COME_COVF_SCHED
+#define COME_COVF_SCHED 0
+#endif
+#ifndef COME_COVF_BUF
+#define COME_COVF_BUF 1
+#endif
+// k_gmm_cov_fb3: sample weights broadcast through a per-wavefront LDS slot instead of readlane
+#ifndef COME_COVF_WLDS
+#define COME_COVF_WLDS 0
+#endif
+// k_gmm_cov_fb3: diagonal tiles' cross terms as U + U^T (4 instead of 6 MFMAs per diagonal tile)
+#ifndef COME_COVF_SYMU
+#define COME_COVF_SYMU 0
+#endif
+// k_gmm_cov_fb3 timing-only builds (garbage results): 1 = no MFMAs, 2 = no staging arithmetic,
+// 3 = no barriers
+#ifndef COME_COVF_DIAG
+#define COME_COVF_DIAG 0
+#endif
 constexpr int kThreads = 256;
 
 // out[r][c] = sum_j A[r][j] * B(c, j) for the tile, where B(c, j) = Bm[c*d + j] (TRANS=false,

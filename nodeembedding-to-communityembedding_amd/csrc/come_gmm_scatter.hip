@@ -437,6 +437,12 @@ struct CovBf3Tiles {
             for (int n = 0; n < cnt[p]; ++n) need[p][ta[p][n]] = need[p][tb[p][n]] = true;
         }
     }
+    // index of tile n of part p among that part's diagonal tiles
+    constexpr int dslot(int p, int n) const {
+        int c = 0;
+        for (int m = 0; m < n; ++m) c += ta[p][m] == tb[p][m];
+        return c;
+    }
 };
 
 template <int D, int P>
@@ -586,8 +592,295 @@ __global__ void __launch_bounds__(CovBf3<D>::THREADS) __attribute__((amdgpu_wave
         else covbf3_part<D, (C::WPC > 2 ? 3 : 0)>(a, smb, nb, tk, nk, k0, chunk, lane);
         return;
     }
+    // cov16_staging's look-ahead is Cov16<D>::NBUF - 1 blocks, while CovBf3Stage::stage and
+    // covbf3_part index the image buffers by blk % 2 / j & 1: the two must agree
+    static_assert(Cov16<D>::NBUF == 2, "k_gmm_cov_bf3 assumes two image buffers");
     CovBf3Stage<D> sg(a, tid - 64 * C::AW, lane, k0, nk, c0, c1);
     cov16_staging<D>(reinterpret_cast<float *>(smb), sg, nb);
+}
+
+// ---- M-step scatter with the staging inside the MFMA wavefronts (k_gmm_cov_fb3, d = 128) -------
+//
+// k_gmm_cov_bf3's arithmetic (E = sqrt(r) (x - m) as three bf16 parts, six exact part products per
+// multiply-add on 32x32x16 bf16 MFMAs, the 10 upper 32x32 tiles) without specialised wavefronts:
+// each of the 4 wavefronts (one per SIMD) owns 5 tiles of one of the workgroup's 2 components AND
+// stages one granule (8 samples of one feature) of the next block for both components, so a
+// SIMD's staging VALU issues in the gaps of its own MFMA stream (a 32x32x16 MFMA holds the SIMD's
+// vector issue for 8 of its 32 cycles; ~4.5 staging VALU per MFMA fit beside it) instead of
+// competing with it from other wavefronts.  Blocks are 16 samples (one k-step), so a workgroup
+// holds 48 KB of LDS and two run per CU: one's barrier waits fill with the other's MFMAs.
+// Image rows are 16 samples (32 B, two 16-B granules swapped by CovFb3::swz: the 16-lane
+// ds_read_b128 fragment groups and the 8-lane ds_write_b128 groups are conflict-free).
+template <int D>
+struct CovFb3 {
+    static_assert(D == 128, "k_gmm_cov_fb3 covers d = 128 (k_gmm_cov_bf3 takes d = 64)");
+    static constexpr int RB = 16;                // samples per block (one k-step)
+    static constexpr int CPW = 2;                // components per workgroup
+    static constexpr int THREADS = 256;          // wavefront w: component w / 2, tiles part w % 2
+    static constexpr int NF = D / 32;            // 32-feature fragments
+    static constexpr int PLANE = D * RB * 2;     // bytes per part image (4 KB)
+    static constexpr int IMG = 3 * PLANE;        // per component
+    static constexpr int BUF = CPW * IMG;        // 24 KB
+    static constexpr int LDS_IMAGES = 2 * BUF;   // 48 KB
+    static constexpr int LDS_BYTES = LDS_IMAGES + (COME_COVF_WLDS ? 4 * 256 : 0);
+    static constexpr int NS = COME_COVF_NS;      // staging register sets (loads NS blocks ahead)
+    // granule swizzle bit of row f: bit 2 ^ bit 3.  Distinct (row mod 8, granule) over the rows of
+    // every ds_read_b128 lane group ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32:
+    // 256-B bank window) and distinct 16-B pieces over every 8-lane ds_write_b128 group of 8
+    // consecutive rows (128-B window)
+    __host__ __device__ static constexpr int swz(int f) { return ((f >> 2) ^ (f >> 3)) & 1; }
+    __host__ __device__ static constexpr int at(int P, int f, int g) {
+        return P * PLANE + f * (RB * 2) + 16 * (g ^ swz(f));
+    }
+};
+
+template <int D, int P>
+__device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb, int k0, int nk,
+                                            int64_t c0, int64_t c1, int64_t chunk, int wid,
+                                            int lane) {
+    using C = CovFb3<D>;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr CovBf3Tiles<D> TT{};
+    constexpr int NT = TT.cnt[P], NS = C::NS;
+    const int tk = wid >> 1;
+    const int i = lane & 31, h = lane >> 5;
+    // staging role: feature f of granule g (samples 8 g .. 8 g + 7 of each block), both components.
+    // Weights come NS blocks at a time: lane l holds r of (block slot min(l / 16, NS - 1), component
+    // l / 8 % 2, sample 8 g + l % 8), square-rooted once per NS blocks and broadcast by readlane.
+    const int f = 64 * (wid & 1) + lane, g = wid >> 1;
+    const int wslot = min(lane >> 4, NS - 1), wk = (lane >> 3) & 1, wsmp = 8 * g + (lane & 7);
+    float mu[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + f] : 0.0f;
+    float xv[NS][8];
+    const int64_t last = c1 - 1;
+    // x rows are wave-uniform: a scalar row address (32-bit row arithmetic within the chunk: the
+    // 64-bit min would go to the VALU) plus the lane's 32-bit feature offset
+    const float *xc = a.x + c0 * D;
+    const int lastr = (int)(c1 - c0) - 1;
+#if COME_COVF_BUF
+    // buffer loads over the chunk (the host keeps a chunk under 2 GB): the row offset goes in
+    // soffset, the lane's feature offset in voffset -- no per-load address VALU
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(xc), 0, (int)((c1 - c0) * D * (int64_t)sizeof(float)), 0x00020000);
+    auto load = [&](int u, int blk) {
+        const int b = blk * C::RB + 8 * g;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            xv[u][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     xr, 4 * f, min(b + q, lastr) * D * 4, 0));
+    };
+#else
+    auto load = [&](int u, int blk) {
+        const int b = blk * C::RB + 8 * g;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xv[u][q] = (xc + (int64_t)min(b + q, lastr) * D)[(uint32_t)f];
+    };
+#endif
+    // the raw weights of the NS blocks first + 1 .. first + NS (slot s: block first + 1 + s)
+    auto wload = [&](int first) -> float {
+        const int64_t row = c0 + (int64_t)(first + 1 + wslot) * C::RB + wsmp;
+        return a.resp[min(row, last) * a.K + min(k0 + wk, a.K - 1)];
+    };
+    // sqrt(r), 0 past the chunk or K (so those E values are exact zeros with no per-element select)
+    auto wfinish = [&](float r, int first) -> float {
+        float w = sqrtf(r);
+        asm volatile("" : "+v"(w));  // computed unconditionally: no branch around the sqrt
+        const int64_t row = c0 + (int64_t)(first + 1 + wslot) * C::RB + wsmp;
+        return (wk < nk && row < c1) ? w : 0.0f;
+    };
+    // the 16 weights of one block (component kk, sample s at 8 kk + s) as per-lane values
+    struct W16 {
+        float v[16];
+    };
+#if COME_COVF_WLDS
+    // through a 256-B LDS slot of the wavefront's own (written once per NS blocks, read back as
+    // four broadcast ds_read_b128 per block: no cross-wavefront traffic, no barrier)
+    float *wslot_lds = reinterpret_cast<float *>(smb + C::LDS_IMAGES) + 64 * wid;
+    auto wpublish = [&](float w) { wslot_lds[lane] = w; };
+    auto wget = [&](float, int slot) -> W16 {
+        W16 r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 t = reinterpret_cast<const float4 *>(wslot_lds + 16 * slot)[q];
+            r.v[4 * q] = t.x, r.v[4 * q + 1] = t.y, r.v[4 * q + 2] = t.z, r.v[4 * q + 3] = t.w;
+        }
+        return r;
+    };
+#else
+    auto wpublish = [&](float) {};
+    auto wget = [&](float w, int slot) -> W16 {
+        W16 r;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            r.v[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), 16 * slot + q));
+        return r;
+    };
+#endif
+    auto stage = [&](int u, int blk, const W16 &ws) {
+        char *buf = smb + (blk & 1) * C::BUF;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            uint32_t p1[4], p2[4], p3[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v[2];
+#pragma unroll
+                for (int z = 0; z < 2; ++z) v[z] = ws.v[8 * kk + 2 * e + z] * (xv[u][2 * e + z] - mu[kk]);
+#if COME_COVF_DIAG == 2  // timing only: no staging arithmetic (the raw values stored)
+                p1[e] = p2[e] = p3[e] = __float_as_uint(xv[u][2 * e]);
+                (void)v;
+#else
+                bf16_split3(v[0], v[1], p1[e], p2[e], p3[e]);
+#endif
+            }
+            char *im = buf + kk * C::IMG;
+            *reinterpret_cast<uint4 *>(im + C::at(0, f, g)) = uint4{p1[0], p1[1], p1[2], p1[3]};
+            *reinterpret_cast<uint4 *>(im + C::at(1, f, g)) = uint4{p2[0], p2[1], p2[2], p2[3]};
+            *reinterpret_cast<uint4 *>(im + C::at(2, f, g)) = uint4{p3[0], p3[1], p3[2], p3[3]};
+        }
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[n][e] = 0.0f;
+    // diagonal tiles (COME_COVF_SYMU): the cross terms a1 b2 + a2 b1 + a1 b3 + a3 b1 of a tile on
+    // the diagonal are U + U^T with U = a1 b2 + a1 b3 -- two MFMAs into a second accumulator
+    // instead of four, U^T added once at the end (4 instead of 6 MFMAs per diagonal tile)
+    constexpr int NDG = COME_COVF_SYMU ? 2 : 1;
+    f32x16 accu[NDG];
+#pragma unroll
+    for (int n = 0; n < NDG; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) accu[n][e] = 0.0f;
+    // blocks past nb (up to the next multiple of NS) are zeros: rows clamped, weights 0.  An empty
+    // chunk (nb = 0) loads nothing and writes its zero partial.
+    if (nb > 0) {
+#pragma unroll
+        for (int u = 0; u < NS; ++u) load(u, u);
+        // block 0's weights sit in slot 0 of the group that "ends" at block 0 (first = -1)
+        {
+            const float w0 = wfinish(wload(-1), -1);
+            wpublish(w0);
+            stage(0, 0, wget(w0, 0));
+        }
+        load(0, NS);
+        float wa = wload(0), wb = wload(NS);  // the next two groups, raw
+        __syncthreads();
+        for (int j0 = 0; j0 < nb; j0 += NS) {
+            const float wsq = wfinish(wa, j0);  // blocks j0 + 1 .. j0 + NS
+            wpublish(wsq);
+            wa = wb;
+            wb = wload(j0 + 2 * NS);
+#pragma unroll
+            for (int u = 0; u < NS; ++u) {
+                const int j = j0 + u;  // multiply block j, stage block j + 1 from set (u + 1) % NS
+                const char *im = smb + (j & 1) * C::BUF + tk * C::IMG;
+                bf16x8 F[C::NF][3];
+#pragma unroll
+                for (int fr = 0; fr < C::NF; ++fr) {
+                    if (!TT.need[P][fr]) continue;
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        F[fr][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * fr + i, h));
+                }
+                stage((u + 1) % NS, j + 1, wget(wsq, u));
+                load((u + 1) % NS, j + 1 + NS);
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+#if COME_COVF_DIAG == 1  // timing only: no MFMAs (the fragments still read)
+                    asm volatile("" ::"v"(F[ta][0]), "v"(F[ta][1]), "v"(F[ta][2]), "v"(F[tb][0]),
+                                 "v"(F[tb][1]), "v"(F[tb][2]));
+                    continue;
+#endif
+                    if (COME_COVF_SYMU && ta == tb) {
+                        constexpr int dq = 0;
+                        const int dg = TT.dslot(P, n);
+                        (void)dq;
+                        accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], accu[dg], 0, 0, 0);
+                        accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], accu[dg], 0, 0, 0);
+                        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
+                        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
+                        continue;
+                    }
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][2], F[tb][0], acc[n], 0, 0, 0);
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], acc[n], 0, 0, 0);
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][0], acc[n], 0, 0, 0);
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], acc[n], 0, 0, 0);
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
+                }
+#if COME_COVF_SCHED
+                // the fragment reads first, then one MFMA per ~4 staging VALU
+                __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+#pragma unroll
+                for (int m = 0; m < 6 * NT; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                    if (m % 5 == 4) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    if (m % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                }
+#endif
+#if COME_COVF_DIAG == 3  // timing only: no barrier
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+                __syncthreads();  // block j + 1 staged; block j's buffer free
+#endif
+            }
+        }
+    }
+    if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
+#if COME_COVF_SYMU
+    // diagonal tiles: acc += U + U^T, U^T through a padded 32 x 33 LDS tile of the wavefront's own
+    // (the loop's last barrier retired every image read, so the buffers are free)
+    if (nb > 0) {
+        float *ut = reinterpret_cast<float *>(smb) + wid * (NDG * 32 * 33);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (TT.ta[P][n] != TT.tb[P][n]) continue;
+            const int dg = TT.dslot(P, n);
+            float *u = ut + dg * 32 * 33;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) u[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = accu[dg][r];
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                acc[n][r] += accu[dg][r] + u[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+        }
+    }
+#endif
+    float *out = a.out + (chunk * a.K + k0 + tk) * D * D;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+        const int jj = 32 * tb + i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int ii = 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
+            out[(int64_t)ii * D + jj] = acc[n][r];
+            if (ta != tb) out[(int64_t)jj * D + ii] = acc[n][r];
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(CovFb3<D>::THREADS) __attribute__((amdgpu_waves_per_eu(2)))
+    k_gmm_cov_fb3(CovArgs a) {
+    using C = CovFb3<D>;
+    extern __shared__ __attribute__((aligned(16))) char smb[];
+    const int64_t chunk = blockIdx.y;
+    const int k0 = blockIdx.x * C::CPW;
+    const int nk = a.K - k0 < C::CPW ? a.K - k0 : C::CPW;
+    const int64_t c0 = chunk * a.rows_per_chunk;
+    int64_t c1 = c0 + a.rows_per_chunk;
+    if (c1 > a.V) c1 = a.V;
+    const int nb = c1 > c0 ? (int)((c1 - c0 + C::RB - 1) / C::RB) : 0;
+    const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wid & 1) covfb3_body<D, 1>(a, smb, nb, k0, nk, c0, c1, chunk, wid, lane);
+    else covfb3_body<D, 0>(a, smb, nb, k0, nk, c0, c1, chunk, wid, lane);
 }
 
 // Any d <= 128 on the VALU: thread owns entries tid + 256 q of the d x d output.
@@ -727,9 +1020,24 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     }
     // gmm_cov_async: 4 (default) = k_gmm_cov_bf3 (bf16 parts), 3 = k_gmm_cov16 (fp32 16x16x4)
     const int cv = current_opts().gmm_cov_async;
-    if (cv != 3 && cv != 4)
-        return set_error(COME_E_INVALID, "gmm_cov_async must be 3 or 4 (got %d)", cv);
-    if (mfma && cv == 4) {
+    if (cv < 3 || cv > 5)
+        return set_error(COME_E_INVALID, "gmm_cov_async must be 3, 4 or 5 (got %d)", cv);
+    if (mfma && cv == 5 && d == 128 && per * d * (int64_t)sizeof(float) < (int64_t(1) << 31)) {
+        static bool attr5 = false;
+        if (!attr5) {
+            (void)hipFuncSetAttribute((const void *)k_gmm_cov_fb3<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr5 = true;
+        }
+        hipLaunchKernelGGL(k_gmm_cov_fb3<128>, dim3((K + CovFb3<128>::CPW - 1) / CovFb3<128>::CPW, used),
+                           dim3(CovFb3<128>::THREADS), CovFb3<128>::LDS_BYTES, (hipStream_t)stream, a);
+        rc = hip_error(hipGetLastError(), "k_gmm_cov_fb3 launch");
+        if (rc || used == 1) return rc;
+        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
+        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+    }
+    if (mfma && (cv == 4 || cv == 5)) {
         static bool attr4 = false;
         if (!attr4) {
             for (void (*f)(CovArgs) : {k_gmm_cov_bf3<64>, k_gmm_cov_bf3<128>})

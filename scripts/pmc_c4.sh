@@ -23,7 +23,7 @@ for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
         kn = r.get("Kernel_Name", "")
         for tag in ("k_community_async", "k_community16", "k_community_bf3", "k_gmm_resp16t",
                     "k_gmm_resp_mfma", "k_gmm_cov_async", "k_gmm_cov16", "k_gmm_cov_bf3",
-                    "k_gmm_resp_bf3", "k_community_b16", "k_gmm_resp_b16"):
+                    "k_gmm_resp_bf3", "k_community_b16", "k_gmm_resp_b16", "k_gmm_cov_fb3"):
             if tag in kn:
                 key = (tag, r["Counter_Name"])
                 agg[key] += float(r["Counter_Value"])

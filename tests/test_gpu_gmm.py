@@ -153,7 +153,7 @@ def test_variant_options_outside_the_kept_set_are_rejected():
         with opts(gmm_resp16=bad):
             with pytest.raises(_lib.ComeError, match="gmm_resp16"):
                 gmm.estep(X, P, mp, ln)
-    for bad in (0, 1, 2, 5):
+    for bad in (0, 1, 2, 6):
         with opts(gmm_cov_async=bad):
             with pytest.raises(_lib.ComeError, match="gmm_cov_async"):
                 gmm.scatter(X, R, mp)
