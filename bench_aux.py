@@ -181,8 +181,8 @@ def c4(args):
     tri_resp = (tri16 if opts.gmm_resp16 == 2 else (ct * (ct + 1)) / (2 * ct * ct)) if ct16 \
         else 1.0
     tri_cov = (tri16 if opts.gmm_cov_async == 3 else tri) if ct16 else 1.0
-    cov_kernel = {3: "k_gmm_cov16", 4: "k_gmm_cov_bf3",
-                  5: "k_gmm_cov_fb3" if d == 128 else "k_gmm_cov_bf3"}[
+    cov_kernel = {3: "k_gmm_cov16", 4: "k_gmm_cov_fb3" if d == 128 else "k_gmm_cov_bf3",
+                  5: "k_gmm_cov_bf3"}[
         opts.gmm_cov_async] if ct16 else "VALU"
     comm_kernel = {2: "k_community16", 3: "k_community_b16"}[
         opts.community_async] if ct16 else "VALU"

@@ -33,7 +33,11 @@
 extern "C" {
 #endif
 
-/* ABI 4 (this header): the launch options "community_async" accept 2 / 3, "gmm_cov_async" 3 / 4
+/* ABI 5 (this header): "gmm_cov_async" accepts 3 / 4 / 5.  Its default 4 now runs k_gmm_cov_fb3 at
+ * d = 128 (the staging inside the MFMA wavefronts; the diagonal 32x32 tiles' cross terms taken as
+ * U + U^T, so their fp32 rounding differs from ABI 4's at the same fp32-level error; off-diagonal
+ * tiles are bit-identical) and k_gmm_cov_bf3 at d = 64; 5 runs ABI 4's k_gmm_cov_bf3 at both widths.
+ * ABI 4: the launch options "community_async" accept 2 / 3, "gmm_cov_async" 3 / 4
  * and "gmm_resp16" 2 / 3 only -- the 32x32 fp32 fallbacks that ABI 3's values 1 / 1 / 0 selected
  * were removed (COME_E_INVALID at the call now) -- and their defaults became the bf16-part MFMA
  * kernels (3 / 4 / 3: fp32 operands as three bf16 parts, fp32-level error).
@@ -44,7 +48,7 @@ extern "C" {
  * contended-row bitmap from the table" (ABI 1: every row cold; now COME_HOT_NONE); the launch
  * options "o2_plain_writeback" and "o2_pair_atomics" (ABI 1, ring-kernel Hogwild) were removed and
  * come_set_option rejects them; o2_kernel = 2 with COME_MODE_HOGWILD returns COME_E_INVALID. */
-#define COME_ABI_VERSION 4
+#define COME_ABI_VERSION 5
 
 enum {
     COME_OK = 0,
@@ -279,11 +283,14 @@ int come_delta_scatter(float *W, float *S, const int64_t *idx, int64_t n, int d,
  *                       MFMAs -- fp32-level error, tests/test_gpu_c4.py; 6.75 vs 11.5 ms at C4);
  *                       2 = k_community16 (fp32 16x16x4 MFMAs, one 16-row tile per wavefront;
  *                       11.5 ms).  Other values: COME_E_INVALID
- *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 4 = k_gmm_cov_bf3 (E^T E with
- *                       E = sqrt(r) (x - m) carried as three bf16 parts, six exact part products
- *                       per multiply-add on 32x32x16 bf16 MFMAs, 10 upper 32x32 tiles; 5.3 ms at
- *                       C4); 3 = k_gmm_cov16 (fp32 16x16x4 tiles: 36 of 64 upper tiles at d =
- *                       128; 7.22 ms).  Other values: COME_E_INVALID
+ *   gmm_cov_async       GMM M-step scatter at d = 64, 128: default 4 = k_gmm_cov_fb3 at d = 128
+ *                       (E^T E with E = sqrt(r) (x - m) carried as three bf16 parts, six exact
+ *                       part products per multiply-add on 32x32x16 bf16 MFMAs -- four on the
+ *                       diagonal tiles, whose cross terms are U + U^T -- the staging inside the
+ *                       MFMA wavefronts; 4.6 ms at C4) and k_gmm_cov_bf3 at d = 64 (specialised
+ *                       staging wavefronts); 5 = k_gmm_cov_bf3 at both widths (5.5 ms at C4);
+ *                       3 = k_gmm_cov16 (fp32 16x16x4 tiles: 36 of 64 upper tiles at d = 128;
+ *                       7.22 ms).  Other values: COME_E_INVALID
  *   walk_staged         default 1: LDS-staged walker output (2 = 8-step, 3 = 32-step slices);
  *                       0 = one store per lane per step (identical walks)
  *   o2_fresh_loads      direct kernel: rows read with agent-scope loads (bypass the CU's L1)

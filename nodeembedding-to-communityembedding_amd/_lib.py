@@ -15,7 +15,7 @@ MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
 TABLE_PACKED = 0x100  # COME_TABLE_PACKED mode flag
 HOT_NONE = 0x200      # COME_HOT_NONE mode flag
-ABI_VERSION = 4       # COME_ABI_VERSION this binding is written for
+ABI_VERSION = 5       # COME_ABI_VERSION this binding is written for
 
 # Every symbol include/come.h declares (checked by tests/test_capi.py).
 SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",

@@ -1,9 +1,9 @@
 // come_gmm_scatter.hip -- GMM M-step scatter matrices (gfx950).
 //
 // Replaces the numerator of sklearn's _estimate_gaussian_covariances_full (community_embeddings.py
-// :27 fit): come_gmm_scatter -> k_gmm_cov_bf3 (default, fp32 operands as bf16 parts), k_gmm_cov16
-// (fp32 MFMA), k_gmm_cov_valu / k_gmm_cov_wide (VALU, any d), k_gmm_cov_reduce (chunk partials in a
-// fixed order).
+// :27 fit): come_gmm_scatter -> k_gmm_cov_fb3 (default at d = 128) and k_gmm_cov_bf3 (d = 64; fp32
+// operands as bf16 parts), k_gmm_cov16 (fp32 MFMA), k_gmm_cov_valu / k_gmm_cov_wide (VALU, any d),
+// k_gmm_cov_reduce (chunk partials in a fixed order).
 
 #include "come_c4.h"
 
@@ -621,8 +621,7 @@ struct CovFb3 {
     static constexpr int PLANE = D * RB * 2;     // bytes per part image (4 KB)
     static constexpr int IMG = 3 * PLANE;        // per component
     static constexpr int BUF = CPW * IMG;        // 24 KB
-    static constexpr int LDS_IMAGES = 2 * BUF;   // 48 KB
-    static constexpr int LDS_BYTES = LDS_IMAGES + (COME_COVF_WLDS ? 4 * 256 : 0);
+    static constexpr int LDS_BYTES = 2 * BUF;    // 48 KB
     static constexpr int NS = COME_COVF_NS;      // staging register sets (loads NS blocks ahead)
     // granule swizzle bit of row f: bit 2 ^ bit 3.  Distinct (row mod 8, granule) over the rows of
     // every ds_read_b128 lane group ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32:
@@ -694,22 +693,6 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
     struct W16 {
         float v[16];
     };
-#if COME_COVF_WLDS
-    // through a 256-B LDS slot of the wavefront's own (written once per NS blocks, read back as
-    // four broadcast ds_read_b128 per block: no cross-wavefront traffic, no barrier)
-    float *wslot_lds = reinterpret_cast<float *>(smb + C::LDS_IMAGES) + 64 * wid;
-    auto wpublish = [&](float w) { wslot_lds[lane] = w; };
-    auto wget = [&](float, int slot) -> W16 {
-        W16 r;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 t = reinterpret_cast<const float4 *>(wslot_lds + 16 * slot)[q];
-            r.v[4 * q] = t.x, r.v[4 * q + 1] = t.y, r.v[4 * q + 2] = t.z, r.v[4 * q + 3] = t.w;
-        }
-        return r;
-    };
-#else
-    auto wpublish = [&](float) {};
     auto wget = [&](float w, int slot) -> W16 {
         W16 r;
 #pragma unroll
@@ -717,7 +700,6 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
             r.v[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), 16 * slot + q));
         return r;
     };
-#endif
     auto stage = [&](int u, int blk, const W16 &ws) {
         char *buf = smb + (blk & 1) * C::BUF;
 #pragma unroll
@@ -755,6 +737,49 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
     for (int n = 0; n < NDG; ++n)
 #pragma unroll
         for (int e = 0; e < 16; ++e) accu[n][e] = 0.0f;
+    // the fragments of block blk (its LDS buffer blk & 1) and the block's MFMAs
+    auto read_frags = [&](bf16x8 (&F)[C::NF][3], int blk) {
+        const char *im = smb + (blk & 1) * C::BUF + tk * C::IMG;
+#pragma unroll
+        for (int fr = 0; fr < C::NF; ++fr) {
+            if (!TT.need[P][fr]) continue;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                F[fr][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * fr + i, h));
+        }
+    };
+    auto mfma_block = [&](const bf16x8 (&F)[C::NF][3]) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int ta = TT.ta[P][n], tb = TT.tb[P][n];
+#if COME_COVF_DIAG == 1  // timing only: no MFMAs (the fragments still read)
+            asm volatile("" ::"v"(F[ta][0]), "v"(F[ta][1]), "v"(F[ta][2]), "v"(F[tb][0]),
+                         "v"(F[tb][1]), "v"(F[tb][2]));
+            continue;
+#endif
+            if (COME_COVF_SYMU && ta == tb) {
+                const int dg = TT.dslot(P, n);
+                accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], accu[dg], 0, 0, 0);
+                accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], accu[dg], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
+                continue;
+            }
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][2], F[tb][0], acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][0], acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
+        }
+    };
+    auto block_barrier = [&]() {
+#if COME_COVF_DIAG == 3  // timing only: no barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+        __syncthreads();
+#endif
+    };
     // blocks past nb (up to the next multiple of NS) are zeros: rows clamped, weights 0.  An empty
     // chunk (nb = 0) loads nothing and writes its zero partial.
     if (nb > 0) {
@@ -763,73 +788,24 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
         // block 0's weights sit in slot 0 of the group that "ends" at block 0 (first = -1)
         {
             const float w0 = wfinish(wload(-1), -1);
-            wpublish(w0);
             stage(0, 0, wget(w0, 0));
         }
         load(0, NS);
         float wa = wload(0), wb = wload(NS);  // the next two groups, raw
-        __syncthreads();
+        block_barrier();
         for (int j0 = 0; j0 < nb; j0 += NS) {
             const float wsq = wfinish(wa, j0);  // blocks j0 + 1 .. j0 + NS
-            wpublish(wsq);
             wa = wb;
             wb = wload(j0 + 2 * NS);
 #pragma unroll
             for (int u = 0; u < NS; ++u) {
                 const int j = j0 + u;  // multiply block j, stage block j + 1 from set (u + 1) % NS
-                const char *im = smb + (j & 1) * C::BUF + tk * C::IMG;
                 bf16x8 F[C::NF][3];
-#pragma unroll
-                for (int fr = 0; fr < C::NF; ++fr) {
-                    if (!TT.need[P][fr]) continue;
-#pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        F[fr][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * fr + i, h));
-                }
+                read_frags(F, j);
                 stage((u + 1) % NS, j + 1, wget(wsq, u));
                 load((u + 1) % NS, j + 1 + NS);
-#pragma unroll
-                for (int n = 0; n < NT; ++n) {
-                    const int ta = TT.ta[P][n], tb = TT.tb[P][n];
-#if COME_COVF_DIAG == 1  // timing only: no MFMAs (the fragments still read)
-                    asm volatile("" ::"v"(F[ta][0]), "v"(F[ta][1]), "v"(F[ta][2]), "v"(F[tb][0]),
-                                 "v"(F[tb][1]), "v"(F[tb][2]));
-                    continue;
-#endif
-                    if (COME_COVF_SYMU && ta == tb) {
-                        constexpr int dq = 0;
-                        const int dg = TT.dslot(P, n);
-                        (void)dq;
-                        accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], accu[dg], 0, 0, 0);
-                        accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], accu[dg], 0, 0, 0);
-                        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
-                        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
-                        continue;
-                    }
-                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][2], F[tb][0], acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][1], acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][1], F[tb][0], acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][1], acc[n], 0, 0, 0);
-                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
-                }
-#if COME_COVF_SCHED
-                // the fragment reads first, then one MFMA per ~4 staging VALU
-                __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-#pragma unroll
-                for (int m = 0; m < 6 * NT; ++m) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-                    if (m % 5 == 4) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                    if (m % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-                }
-#endif
-#if COME_COVF_DIAG == 3  // timing only: no barrier
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-                __syncthreads();  // block j + 1 staged; block j's buffer free
-#endif
+                mfma_block(F);
+                block_barrier();  // block j + 1 staged; block j's buffer free
             }
         }
     }
@@ -1018,11 +994,13 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
         return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
     }
-    // gmm_cov_async: 4 (default) = k_gmm_cov_bf3 (bf16 parts), 3 = k_gmm_cov16 (fp32 16x16x4)
+    // gmm_cov_async: 4 (default) = k_gmm_cov_fb3 at d = 128 / k_gmm_cov_bf3 at d = 64 (bf16 parts),
+    // 5 = k_gmm_cov_bf3 at both widths, 3 = k_gmm_cov16 (fp32 16x16x4)
     const int cv = current_opts().gmm_cov_async;
     if (cv < 3 || cv > 5)
         return set_error(COME_E_INVALID, "gmm_cov_async must be 3, 4 or 5 (got %d)", cv);
-    if (mfma && cv == 5 && d == 128 && per * d * (int64_t)sizeof(float) < (int64_t(1) << 31)) {
+    // 4 at d = 128 (chunks under 2 GB): k_gmm_cov_fb3; 4 at d = 64, and 5: k_gmm_cov_bf3
+    if (mfma && cv == 4 && d == 128 && per * d * (int64_t)sizeof(float) < (int64_t(1) << 31)) {
         static bool attr5 = false;
         if (!attr5) {
             (void)hipFuncSetAttribute((const void *)k_gmm_cov_fb3<128>,

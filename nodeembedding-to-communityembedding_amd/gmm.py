@@ -103,8 +103,9 @@ def resp_sum(resp, chunks=256):
 
 def scatter_chunks(V, K, d, cus):
     """Row chunks of the scatter's grid.  The MFMA kernels (d = 64, 128) run (K / components per
-    workgroup) x chunks workgroups, two resident per CU (k_gmm_cov16; k_gmm_cov_bf3 holds one, so
-    the same count is twice as many rounds of half the slots): the chunk count makes that a whole
+    workgroup) x chunks workgroups, two resident per CU (k_gmm_cov16, k_gmm_cov_fb3; k_gmm_cov_bf3
+    holds one, so the same count is twice as many rounds of half the slots): the chunk count makes
+    that a whole
     number of rounds of the 2 x CUs slots, 8 of them (~4k workgroups: enough to even out, the partials
     <= 512 MB).  A ragged last round costs its whole length: at C4 (25 component pairs) 163
     chunks = 7.96 rounds ran 7.44 ms, 168 (-> 169 used) = 8.25 rounds 7.75 ms

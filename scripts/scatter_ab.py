@@ -1,7 +1,7 @@
 """Interleaved A/B of the GMM M-step scatter kernels at C4 (V = 1M, K = 50, d = 128) in ONE
 process: each variant is a value of the launch option gmm_cov_async (3 = k_gmm_cov16 fp32,
-4 = k_gmm_cov_bf3, 5 = k_gmm_cov_fb3), optionally with an alternative libcome.so per variant
-("5@path/to/libcome_x.so" is not supported: one library per process -- use COME_LIB_PATH).
+4 = k_gmm_cov_fb3, 5 = k_gmm_cov_bf3); an alternative build goes in COME_LIB_PATH (one library
+per process).
 Per variant: median / min of the HIP-event time of gmm.scatter (kernel + chunk reduction) over
 interleaved rounds, the max |diff| against the first variant relative to max |S|, a digest of the
 output bytes (bit identity), and the RMS / max relative error against float64 on the first

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.come_abi_version() == _lib.ABI_VERSION == 4
+    assert L.come_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_library_is_the_build_of_the_sources_beside_it(monkeypatch):

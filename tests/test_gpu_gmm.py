@@ -265,19 +265,20 @@ def test_community2vec_distributed_flag_single_process_matches():
                                           (5000, 3, 64, None), (65, 4, 64, 2), (700, 1, 128, 3),
                                           (517, 7, 64, 2), (1031, 9, 64, None)])
 def test_scatter_default_and_fallback_agree(V, K, d, chunks):
-    """The fp32 k_gmm_cov16 (16x16x4 tiles) and the bf16-part k_gmm_cov_bf3 (E^T E, E = sqrt(r)
-    (x - m); 2 (d=128) / 4 (d=64) components per workgroup, operands centred and weighted once
-    per block into transposed LDS images): equal up to the order and form of the products (atol
-    1e-5 of the matrix scale), symmetric (off-diagonal tiles are stored transposed; inside a
-    diagonal tile (w x_a) x_b and (w x_b) x_a round apart, as sklearn's np.dot(resp * diff.T,
-    diff) does).  K not a multiple of the components per workgroup included."""
+    """The fp32 k_gmm_cov16 (16x16x4 tiles) and the bf16-part kernels (E^T E, E = sqrt(r) (x - m):
+    option 4 = k_gmm_cov_fb3 at d = 128 / k_gmm_cov_bf3 at d = 64, option 5 = k_gmm_cov_bf3; 2
+    (d=128) / 4 (d=64) components per workgroup, operands centred and weighted once per block into
+    transposed LDS images): equal up to the order and form of the products (atol 1e-5 of the
+    matrix scale), symmetric (off-diagonal tiles are stored transposed; inside a diagonal tile
+    (w x_a) x_b and (w x_b) x_a round apart, as sklearn's np.dot(resp * diff.T, diff) does).  K
+    not a multiple of the components per workgroup included."""
     rng = np.random.RandomState(V + K + d)
     t = lambda a: torch.as_tensor(a, device=dev())  # noqa: E731
     x = t(rng.standard_normal((V, d)).astype(np.float32))
     resp = t(rng.dirichlet(np.ones(K), V).astype(np.float32))
     mu = t(rng.standard_normal((K, d)).astype(np.float32))
     out = []
-    for opt in (3, 4):
+    for opt in (3, 4, 5):
         with opts(gmm_cov_async=opt):
             out.append(gmm.scatter(x, resp, mu, chunks=chunks).cpu().numpy())
     for o in out[1:]:
