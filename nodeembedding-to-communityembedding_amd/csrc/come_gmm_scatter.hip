@@ -945,14 +945,49 @@ __global__ void __launch_bounds__(kThreads) k_gmm_cov_wide(CovArgs a) {
     }
 }
 
-// out[i] = sum_c part[c][i] in chunk order (deterministic), i over K d^2 entries.
+// out[i] = sum_c part[c][i] in chunk order (deterministic), i over K d^2 entries.  Four entries
+// per thread (16-byte loads when n % 4 == 0) and eight chunks' loads issued ahead of their adds,
+// which stay in chunk order: 534 MB of partials at C4 in 0.17 ms as one dword and one chunk at a
+// time per thread.
+template <bool VEC4>
 __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float *out, int64_t n,
                                                         int chunks) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    float s = 0.0f;
-    for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * n + i];
-    out[i] = s;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // entries 4 q .. 4 q + 3
+    if (4 * q >= n) return;
+    if (VEC4) {
+        const f32x4 *p = reinterpret_cast<const f32x4 *>(part) + q;
+        const int64_t stride = n / 4;
+        f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
+        int c = 0;
+        for (; c + 8 <= chunks; c += 8) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(c + u) * stride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; c < chunks; ++c) s += p[(int64_t)c * stride];
+        reinterpret_cast<f32x4 *>(out)[q] = s;
+    } else {
+        for (int64_t i = 4 * q; i < 4 * q + 4 && i < n; ++i) {
+            float s = 0.0f;
+            for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * n + i];
+            out[i] = s;
+        }
+    }
+}
+
+static int launch_cov_reduce(const float *part, float *out, int64_t n, int chunks,
+                             hipStream_t stream) {
+    const unsigned grid = (unsigned)((n + 1023) / 1024);
+    if (n % 4 == 0)
+        hipLaunchKernelGGL(k_gmm_cov_reduce<true>, dim3(grid), dim3(256), 0, stream, part, out, n,
+                           chunks);
+    else
+        hipLaunchKernelGGL(k_gmm_cov_reduce<false>, dim3(grid), dim3(256), 0, stream, part, out, n,
+                           chunks);
+    return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
 }
 
 }  // namespace come
@@ -990,9 +1025,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, a);
         rc = hip_error(hipGetLastError(), "k_gmm_cov_wide launch");
         if (rc || used == 1) return rc;
-        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
-        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+        return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
     }
     // gmm_cov_async: 4 (default) = k_gmm_cov_fb3 at d = 128 / k_gmm_cov_bf3 at d = 64 (bf16 parts),
     // 5 = k_gmm_cov_bf3 at both widths, 3 = k_gmm_cov16 (fp32 16x16x4)
@@ -1011,9 +1044,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            dim3(CovFb3<128>::THREADS), CovFb3<128>::LDS_BYTES, (hipStream_t)stream, a);
         rc = hip_error(hipGetLastError(), "k_gmm_cov_fb3 launch");
         if (rc || used == 1) return rc;
-        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
-        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+        return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
     }
     if (mfma && (cv == 4 || cv == 5)) {
         static bool attr4 = false;
@@ -1031,9 +1062,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, a);
         rc = hip_error(hipGetLastError(), "k_gmm_cov_bf3 launch");
         if (rc || used == 1) return rc;
-        hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                           (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
-        return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+        return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
     }
     void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu : (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>);
     const int threads = !mfma ? 256 : (d == 64 ? Cov16<64>::THREADS : Cov16<128>::THREADS);
@@ -1042,7 +1071,5 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                        (hipStream_t)stream, a);
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;
-    hipLaunchKernelGGL(k_gmm_cov_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, (const float *)scratch, scatter_out, n, used);
-    return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+    return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
 }
