@@ -105,18 +105,19 @@ def scatter_chunks(V, K, d, cus):
     """Row chunks of the scatter's grid.  The MFMA kernels (d = 64, 128) run (K / components per
     workgroup) x chunks workgroups, two resident per CU (k_gmm_cov16, k_gmm_cov_fb3; k_gmm_cov_bf3
     holds one, so the same count is twice as many rounds of half the slots): the chunk count makes
-    that a whole number of rounds of the 2 x CUs slots, 4 of them (~2k workgroups at C4: enough to
-    even out, and half the partials of 8 rounds -- 267 MB, 0.05 ms less in the chunk reduction:
-    4.537 vs 4.574 ms at C4, profiles/r07_ab_scatter_fused.txt).  A ragged last round costs its
-    whole length: at C4 (25 component pairs) 163 chunks = 7.96 rounds ran 7.44 ms, 168 (-> 169
-    used) = 8.25 rounds 7.75 ms with k_gmm_cov16 (profiles/r05_ab_gmm_diag.txt).  Other widths
-    (the VALU kernel): ~8192 workgroups."""
+    that a whole number of rounds of the 2 x CUs slots, 8 of them (~4k workgroups: enough to even
+    out, the partials <= 512 MB).  A ragged last round costs its whole length: at C4 (25 component
+    pairs) 163 chunks = 7.96 rounds ran 7.44 ms, 168 (-> 169 used) = 8.25 rounds 7.75 ms
+    (profiles/r05_ab_gmm_diag.txt).  Four rounds (81 chunks) ran 0.8% faster with the bf16-part
+    kernels but doubles each chunk's fp32 accumulation: their error against float64 then exceeds
+    1.5x the fp32 kernel's (test_c4_scatter_bf3_error_is_fp32_level; profiles/
+    r07_ab_scatter_fused.txt).  Other widths (the VALU kernel): ~8192 workgroups."""
     cap = max(1, min((128 << 20) // max(1, K * d * d), -(-V // 64)))
     if d not in (64, 128) or cus <= 0:
         return max(1, min(-(-8192 // K), cap))
     groups = -(-K // (2 if d == 128 else 4))
     slots = 2 * cus
-    for rounds in range(4, 0, -1):
+    for rounds in range(8, 0, -1):
         c = rounds * slots // groups
         if 1 <= c <= cap:
             return c
