@@ -53,21 +53,14 @@ constexpr int kTR = 16;        // rows per workgroup tile
 #define COME_COV3_WPC 2
 #endif
 // k_gmm_cov_fb3 (A/B hooks): staging register sets (loads NS blocks ahead; 2: 4.64 vs 4.84 ms with
-// 3 at C4 with SYMU, which at 3 sets needs all 256 VGPRs), buffer loads for x (0: global loads with
-// 64-bit VALU addresses, 4% slower), the diagonal tiles' cross terms as U + U^T (0: six MFMAs per
-// diagonal tile as k_gmm_cov_bf3, bit-identical to it; 1: four, 3-5% faster), and timing-only
-// builds with garbage results (DIAG 1 = no MFMAs, 2 = no staging arithmetic, 3 = no barriers)
+// 3 at C4 with SYMU, which at 3 sets needs all 256 VGPRs) and the diagonal tiles' cross terms as
+// U + U^T (0: six MFMAs per diagonal tile as k_gmm_cov_bf3, bit-identical to it; 1: four, 3-5%
+// faster)
 #ifndef COME_COVF_NS
 #define COME_COVF_NS 2
 #endif
-#ifndef COME_COVF_BUF
-#define COME_COVF_BUF 1
-#endif
 #ifndef COME_COVF_SYMU
 #define COME_COVF_SYMU 1
-#endif
-#ifndef COME_COVF_DIAG
-#define COME_COVF_DIAG 0
 #endif
 constexpr int kThreads = 256;
 

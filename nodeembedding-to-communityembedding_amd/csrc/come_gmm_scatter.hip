@@ -604,13 +604,16 @@ __global__ void __launch_bounds__(CovBf3<D>::THREADS) __attribute__((amdgpu_wave
 // k_gmm_cov_bf3's arithmetic (E = sqrt(r) (x - m) as three bf16 parts, six exact part products per
 // multiply-add on 32x32x16 bf16 MFMAs, the 10 upper 32x32 tiles) without specialised wavefronts:
 // each of the 4 wavefronts (one per SIMD) owns 5 tiles of one of the workgroup's 2 components AND
-// stages one granule (8 samples of one feature) of the next block for both components, so a
-// SIMD's staging VALU issues in the gaps of its own MFMA stream (a 32x32x16 MFMA holds the SIMD's
-// vector issue for 8 of its 32 cycles; ~4.5 staging VALU per MFMA fit beside it) instead of
-// competing with it from other wavefronts.  Blocks are 16 samples (one k-step), so a workgroup
-// holds 48 KB of LDS and two run per CU: one's barrier waits fill with the other's MFMAs.
-// Image rows are 16 samples (32 B, two 16-B granules swapped by CovFb3::swz: the 16-lane
-// ds_read_b128 fragment groups and the 8-lane ds_write_b128 groups are conflict-free).
+// stages one sample x 8 features of the next block for both components, so a SIMD's staging VALU
+// issues in the gaps of its own MFMA stream (a 32x32x16 MFMA holds the SIMD's vector issue for 8
+// of its 32 cycles) instead of competing with it from other wavefronts.  Blocks are 16 samples
+// (one k-step), so a workgroup holds 48 KB of LDS and two run per CU: one's barrier waits fill
+// with the other's MFMAs.  The images are sample-major (row = sample: 128 features x 2 B per part)
+// and the MFMA fragments are read with ds_read_b64_tr_b16 (a 16-lane group receives a 4-sample x
+// 16-feature block transposed: lane i gets feature i of the 4 samples), so a staging lane's weight
+// is its own sample's (no broadcast) and its x is two 16-byte loads.  Diagonal tiles take their
+// cross terms a1 b2 + a2 b1 + a1 b3 + a3 b1 as U + U^T, U = a1 b2 + a1 b3: four MFMAs instead of six,
+// U^T added once at the end (COME_COVF_SYMU).
 template <int D>
 struct CovFb3 {
     static_assert(D == 128, "k_gmm_cov_fb3 covers d = 128 (k_gmm_cov_bf3 takes d = 64)");
@@ -623,104 +626,76 @@ struct CovFb3 {
     static constexpr int BUF = CPW * IMG;        // 24 KB
     static constexpr int LDS_BYTES = 2 * BUF;    // 48 KB
     static constexpr int NS = COME_COVF_NS;      // staging register sets (loads NS blocks ahead)
-    // granule swizzle bit of row f: bit 2 ^ bit 3.  Distinct (row mod 8, granule) over the rows of
-    // every ds_read_b128 lane group ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32:
-    // 256-B bank window) and distinct 16-B pieces over every 8-lane ds_write_b128 group of 8
-    // consecutive rows (128-B window)
-    __host__ __device__ static constexpr int swz(int f) { return ((f >> 2) ^ (f >> 3)) & 1; }
-    __host__ __device__ static constexpr int at(int P, int f, int g) {
-        return P * PLANE + f * (RB * 2) + 16 * (g ^ swz(f));
+    // chunk ch (16 B, 8 features) of sample row r of part P: chunks XOR-swizzled by the row, so each
+    // tr read's 32-lane half (4 rows x 4 chunks x two 8-B halves: 256 B) and each 8-lane
+    // ds_write_b128 group (8 chunks of one row: 128 B) cover distinct banks
+    __host__ __device__ static constexpr int at(int P, int r, int ch) {
+        return P * PLANE + r * (D * 2) + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
     }
 };
 
 template <int D, int P>
 __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb, int k0, int nk,
-                                            int64_t c0, int64_t c1, int64_t chunk, int wid,
-                                            int lane) {
+                                               int64_t c0, int64_t c1, int64_t chunk, int wid,
+                                               int lane) {
     using C = CovFb3<D>;
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
     constexpr CovBf3Tiles<D> TT{};
     constexpr int NT = TT.cnt[P], NS = C::NS;
     const int tk = wid >> 1;
     const int i = lane & 31, h = lane >> 5;
-    // staging role: feature f of granule g (samples 8 g .. 8 g + 7 of each block), both components.
-    // Weights come NS blocks at a time: lane l holds r of (block slot min(l / 16, NS - 1), component
-    // l / 8 % 2, sample 8 g + l % 8), square-rooted once per NS blocks and broadcast by readlane.
-    const int f = 64 * (wid & 1) + lane, g = wid >> 1;
-    const int wslot = min(lane >> 4, NS - 1), wk = (lane >> 3) & 1, wsmp = 8 * g + (lane & 7);
-    float mu[2];
+    // staging role: sample s = 4 wid + lane / 16 of each block, features 8 ch .. 8 ch + 7
+    const int s = 4 * wid + (lane >> 4), ch = lane & 15;
+    float mu[2][8];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) mu[kk] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + f] : 0.0f;
-    float xv[NS][8];
-    const int64_t last = c1 - 1;
-    // x rows are wave-uniform: a scalar row address (32-bit row arithmetic within the chunk: the
-    // 64-bit min would go to the VALU) plus the lane's 32-bit feature offset
-    const float *xc = a.x + c0 * D;
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            mu[kk][e] = kk < nk ? a.means[(int64_t)(k0 + kk) * D + 8 * ch + e] : 0.0f;
+    f32x4 xv[NS][2];
+    float rv[NS][2];
     const int lastr = (int)(c1 - c0) - 1;
-#if COME_COVF_BUF
-    // buffer loads over the chunk (the host keeps a chunk under 2 GB): the row offset goes in
-    // soffset, the lane's feature offset in voffset -- no per-load address VALU
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(xc), 0, (int)((c1 - c0) * D * (int64_t)sizeof(float)), 0x00020000);
+        const_cast<float *>(a.x + c0 * D), 0, (int)((c1 - c0) * D * (int64_t)sizeof(float)),
+        0x00020000);
+    // the chunk's responsibilities rows, as a buffer too (32-bit lane offsets)
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(a.resp + c0 * a.K), 0, (int)((c1 - c0) * a.K * (int64_t)sizeof(float)),
+        0x00020000);
+    const int kc0 = 4 * k0, kc1 = 4 * min(k0 + 1, a.K - 1);
     auto load = [&](int u, int blk) {
-        const int b = blk * C::RB + 8 * g;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            xv[u][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     xr, 4 * f, min(b + q, lastr) * D * 4, 0));
+        const int row = min(blk * C::RB + s, lastr);  // rows clamped to the chunk (zero weight)
+        const int off = row * (D * 4) + 32 * ch;
+        xv[u][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        xv[u][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 0));
+        const int roff = row * a.K * 4;
+        rv[u][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff, kc0, 0));
+        rv[u][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff, kc1, 0));
     };
-#else
-    auto load = [&](int u, int blk) {
-        const int b = blk * C::RB + 8 * g;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) xv[u][q] = (xc + (int64_t)min(b + q, lastr) * D)[(uint32_t)f];
-    };
-#endif
-    // the raw weights of the NS blocks first + 1 .. first + NS (slot s: block first + 1 + s)
-    auto wload = [&](int first) -> float {
-        const int64_t row = c0 + (int64_t)(first + 1 + wslot) * C::RB + wsmp;
-        return a.resp[min(row, last) * a.K + min(k0 + wk, a.K - 1)];
-    };
-    // sqrt(r), 0 past the chunk or K (so those E values are exact zeros with no per-element select)
-    auto wfinish = [&](float r, int first) -> float {
-        float w = sqrtf(r);
-        asm volatile("" : "+v"(w));  // computed unconditionally: no branch around the sqrt
-        const int64_t row = c0 + (int64_t)(first + 1 + wslot) * C::RB + wsmp;
-        return (wk < nk && row < c1) ? w : 0.0f;
-    };
-    // the 16 weights of one block (component kk, sample s at 8 kk + s) as per-lane values
-    struct W16 {
-        float v[16];
-    };
-    auto wget = [&](float w, int slot) -> W16 {
-        W16 r;
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            r.v[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), 16 * slot + q));
-        return r;
-    };
-    auto stage = [&](int u, int blk, const W16 &ws) {
+    auto stage = [&](int u, int blk) {
         char *buf = smb + (blk & 1) * C::BUF;
+        const bool live = blk * C::RB + s <= lastr;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
+            // sqrt(r) by v_sqrt_f32 (within 1 ulp; the correctly rounded sqrtf would add ~16 VALU
+            // per block), 0 past the chunk or K: those E values are exact zeros
+            float w = __builtin_amdgcn_sqrtf(rv[u][kk]);
+            w = live && kk < nk ? w : 0.0f;
             uint32_t p1[4], p2[4], p3[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float v[2];
-#pragma unroll
-                for (int z = 0; z < 2; ++z) v[z] = ws.v[8 * kk + 2 * e + z] * (xv[u][2 * e + z] - mu[kk]);
-#if COME_COVF_DIAG == 2  // timing only: no staging arithmetic (the raw values stored)
-                p1[e] = p2[e] = p3[e] = __float_as_uint(xv[u][2 * e]);
-                (void)v;
-#else
-                bf16_split3(v[0], v[1], p1[e], p2[e], p3[e]);
-#endif
+                const float v0 = w * (xv[u][e >> 1][2 * (e & 1)] - mu[kk][2 * e]);
+                const float v1 = w * (xv[u][e >> 1][2 * (e & 1) + 1] - mu[kk][2 * e + 1]);
+                bf16_split3(v0, v1, p1[e], p2[e], p3[e]);
             }
             char *im = buf + kk * C::IMG;
-            *reinterpret_cast<uint4 *>(im + C::at(0, f, g)) = uint4{p1[0], p1[1], p1[2], p1[3]};
-            *reinterpret_cast<uint4 *>(im + C::at(1, f, g)) = uint4{p2[0], p2[1], p2[2], p2[3]};
-            *reinterpret_cast<uint4 *>(im + C::at(2, f, g)) = uint4{p3[0], p3[1], p3[2], p3[3]};
+            *reinterpret_cast<uint4 *>(im + C::at(0, s, ch)) = uint4{p1[0], p1[1], p1[2], p1[3]};
+            *reinterpret_cast<uint4 *>(im + C::at(1, s, ch)) = uint4{p2[0], p2[1], p2[2], p2[3]};
+            *reinterpret_cast<uint4 *>(im + C::at(2, s, ch)) = uint4{p3[0], p3[1], p3[2], p3[3]};
         }
     };
     f32x16 acc[NT];
@@ -728,35 +703,40 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
     for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[n][e] = 0.0f;
-    // diagonal tiles (COME_COVF_SYMU): the cross terms a1 b2 + a2 b1 + a1 b3 + a3 b1 of a tile on
-    // the diagonal are U + U^T with U = a1 b2 + a1 b3 -- two MFMAs into a second accumulator
-    // instead of four, U^T added once at the end (4 instead of 6 MFMAs per diagonal tile)
     constexpr int NDG = COME_COVF_SYMU ? 2 : 1;
     f32x16 accu[NDG];
 #pragma unroll
     for (int n = 0; n < NDG; ++n)
 #pragma unroll
         for (int e = 0; e < 16; ++e) accu[n][e] = 0.0f;
-    // the fragments of block blk (its LDS buffer blk & 1) and the block's MFMAs
+    // fragment fr of block blk: lane (group g16 = lane / 16, i16 = lane % 16) receives feature
+    // 32 fr + 16 (g16 & 1) + i16 of samples 8 (g16 / 2) + 4 t + 0..3 from read t; it supplies the
+    // address of row 8 (g16 / 2) + 4 t + i16 / 4, features 32 fr + 16 (g16 & 1) + 4 (i16 % 4) .. + 3
+    const int g16 = lane >> 4, i16 = lane & 15;
     auto read_frags = [&](bf16x8 (&F)[C::NF][3], int blk) {
         const char *im = smb + (blk & 1) * C::BUF + tk * C::IMG;
 #pragma unroll
         for (int fr = 0; fr < C::NF; ++fr) {
             if (!TT.need[P][fr]) continue;
+            const int cb = 4 * fr + 2 * (g16 & 1) + ((i16 & 3) >> 1);
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
-                F[fr][p] = *reinterpret_cast<const bf16x8 *>(im + C::at(p, 32 * fr + i, h));
+            for (int p = 0; p < 3; ++p) {
+                s16x4 t2[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int r = 8 * (g16 >> 1) + 4 * t + (i16 >> 2);
+                    const char *ad = im + C::at(p, r, cb) + 8 * (i16 & 1);
+                    t2[t] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(ad));
+                }
+                const uint2 lo = __builtin_bit_cast(uint2, t2[0]), hi = __builtin_bit_cast(uint2, t2[1]);
+                F[fr][p] = __builtin_bit_cast(bf16x8, uint4{lo.x, lo.y, hi.x, hi.y});
+            }
         }
     };
     auto mfma_block = [&](const bf16x8 (&F)[C::NF][3]) {
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int ta = TT.ta[P][n], tb = TT.tb[P][n];
-#if COME_COVF_DIAG == 1  // timing only: no MFMAs (the fragments still read)
-            asm volatile("" ::"v"(F[ta][0]), "v"(F[ta][1]), "v"(F[ta][2]), "v"(F[tb][0]),
-                         "v"(F[tb][1]), "v"(F[tb][2]));
-            continue;
-#endif
             if (COME_COVF_SYMU && ta == tb) {
                 const int dg = TT.dslot(P, n);
                 accu[dg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][2], accu[dg], 0, 0, 0);
@@ -773,46 +753,27 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
             acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[ta][0], F[tb][0], acc[n], 0, 0, 0);
         }
     };
-    auto block_barrier = [&]() {
-#if COME_COVF_DIAG == 3  // timing only: no barrier
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-        __syncthreads();
-#endif
-    };
-    // blocks past nb (up to the next multiple of NS) are zeros: rows clamped, weights 0.  An empty
-    // chunk (nb = 0) loads nothing and writes its zero partial.
     if (nb > 0) {
 #pragma unroll
         for (int u = 0; u < NS; ++u) load(u, u);
-        // block 0's weights sit in slot 0 of the group that "ends" at block 0 (first = -1)
-        {
-            const float w0 = wfinish(wload(-1), -1);
-            stage(0, 0, wget(w0, 0));
-        }
+        stage(0, 0);
         load(0, NS);
-        float wa = wload(0), wb = wload(NS);  // the next two groups, raw
-        block_barrier();
+        __syncthreads();
         for (int j0 = 0; j0 < nb; j0 += NS) {
-            const float wsq = wfinish(wa, j0);  // blocks j0 + 1 .. j0 + NS
-            wa = wb;
-            wb = wload(j0 + 2 * NS);
 #pragma unroll
             for (int u = 0; u < NS; ++u) {
                 const int j = j0 + u;  // multiply block j, stage block j + 1 from set (u + 1) % NS
                 bf16x8 F[C::NF][3];
                 read_frags(F, j);
-                stage((u + 1) % NS, j + 1, wget(wsq, u));
+                stage((u + 1) % NS, j + 1);
                 load((u + 1) % NS, j + 1 + NS);
                 mfma_block(F);
-                block_barrier();  // block j + 1 staged; block j's buffer free
+                __syncthreads();  // block j + 1 staged; block j's buffer free
             }
         }
     }
     if (tk >= nk) return;  // wavefront-uniform: K not a multiple of CPW
 #if COME_COVF_SYMU
-    // diagonal tiles: acc += U + U^T, U^T through a padded 32 x 33 LDS tile of the wavefront's own
-    // (the loop's last barrier retired every image read, so the buffers are free)
     if (nb > 0) {
         float *ut = reinterpret_cast<float *>(smb) + wid * (NDG * 32 * 33);
 #pragma unroll
