@@ -993,8 +993,10 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     const int cv = current_opts().gmm_cov_async;
     if (cv < 3 || cv > 5)
         return set_error(COME_E_INVALID, "gmm_cov_async must be 3, 4 or 5 (got %d)", cv);
-    // 4 at d = 128 (chunks under 2 GB): k_gmm_cov_fb3; 4 at d = 64, and 5: k_gmm_cov_bf3
-    if (mfma && cv == 4 && d == 128 && per * d * (int64_t)sizeof(float) < (int64_t(1) << 31)) {
+    // 4 at d = 128: k_gmm_cov_fb3 (its buffer descriptors span one chunk of x and of resp: each
+    // under 2 GB, else k_gmm_cov_bf3); 4 at d = 64, and 5: k_gmm_cov_bf3
+    const bool fb3_fits = per * std::max(d, K) * (int64_t)sizeof(float) < (int64_t(1) << 31);
+    if (mfma && cv == 4 && d == 128 && fb3_fits) {
         static bool attr5 = false;
         if (!attr5) {
             (void)hipFuncSetAttribute((const void *)k_gmm_cov_fb3<128>,
