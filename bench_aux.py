@@ -214,9 +214,11 @@ def c4(args):
     gm._set_params(t64(w), mu.double(), t64(cov))
     resp0 = pis.contiguous()
 
-    def em_iter():
-        resp, _ = gmm.estep(x0s, gm._e_pc, gm._e_mp, gm._e_ln)
-        gm._set_params(*gm._m_step(x0s, resp))
+    def em_iter():  # one iteration of GaussianMixture.fit's loop, its host read included
+        resp, lse = gmm.estep(x0s, gm._e_pc, gm._e_mp, gm._e_ln)
+        info = gm._m_step_params(x0s, resp)
+        lb_info = torch.stack([lse.double().sum(), (info != 0).any().double()]).cpu()
+        assert lb_info[1] == 0
     el_e, ks_e = timed(em_iter, args.steps, args.warmup)
     el_s, ks_s = timed(lambda: gmm.scatter(x0s, resp0, mu), args.steps, args.warmup)
     te, ts = float(np.mean(ks_e)) / 1e3, float(np.mean(ks_s)) / 1e3

@@ -169,6 +169,19 @@ int come_gmm_estep(const float *x, int64_t V, int d, const float *prec_chol, con
 int come_gmm_scatter(const float *x, int64_t V, int d, const float *resp, const float *means,
                      int K, int chunks, float *scratch, float *scatter_out, void *stream);
 
+/* The rest of one M-step and the E-step parameters it implies, one workgroup per component, in
+ * float64 (sklearn _estimate_gaussian_covariances_full + _compute_precision_cholesky +
+ * _estimate_log_gaussian_prob's constants): cov_out [K x d x d] = scatter_k / nk_k + reg_covar I,
+ * its Cholesky factor L, prec_chol_out [K x d x d] = L^-T (upper), and the E-step's fp32 inputs:
+ * e_prec_chol [K x d x d] = prec_chol, e_mu_prec [K x d] = means_k prec_chol_k, e_log_norm [K] =
+ * log weights_k + sum log diag(prec_chol_k) - d/2 log(2 pi).  info [K] (device int32): 0, or j + 1
+ * when the j-th pivot of component k's Cholesky factorisation is not positive (sklearn raises;
+ * the caller checks).  All pointers are device memory; 1 <= d <= 128. */
+int come_gmm_params(const double *scatter, const double *nk, const double *means,
+                    const double *weights, int K, int d, double reg_covar, double *cov_out,
+                    double *prec_chol_out, float *e_prec_chol, float *e_mu_prec,
+                    float *e_log_norm, int *info, void *stream);
+
 /* ---- Random walks: the producer of train_o2's input (utils/graph_utils.py) ----
  * Graphs are CSR over node POSITIONS 0..V-1 in networkx order (see come_graph_from_edges):
  * rowptr int64 [V+1], col int32 [rowptr[V]] (neighbours in adjacency order).  `emit` (optional,

@@ -25,7 +25,7 @@ SYMBOLS = ("come_abi_version", "come_last_error", "come_init", "come_exp_table",
            "come_pyrandom_draw", "come_np_draw_seeds", "come_graph_from_edges",
            "come_read_int_rows",
            "come_write_int_rows", "come_save_embedding", "come_format_f32",
-           "come_gmm_estep", "come_gmm_scatter", "come_pack_table",
+           "come_gmm_estep", "come_gmm_scatter", "come_gmm_params", "come_pack_table",
            "come_delta_begin", "come_delta_end", "come_get_options", "come_sgns_o2_ex",
            "come_sgns_o1_ex", "come_hot_rows", "come_lcg_table_draws", "come_delta_flags",
            "come_delta_gather", "come_delta_scatter", "come_cpu_sgns_o2", "come_cpu_sgns_o1",
@@ -102,6 +102,7 @@ def lib():
     L.come_delta_end.argtypes = [P, P, P, P, i64, P]
     L.come_gmm_estep.argtypes = [P, i64, i32, P, P, P, i32, P, P, P]
     L.come_gmm_scatter.argtypes = [P, i64, i32, P, P, i32, i32, P, P, P]
+    L.come_gmm_params.argtypes = [P, P, P, P, i32, i32, f64, P, P, P, P, P, P, P]
     L.come_make_table.argtypes = [P, i64, P, u64, f64]
     L.come_count_o2_pairs.argtypes = [P, i64, i32, i32]
     L.come_count_o2_pairs.restype = i64

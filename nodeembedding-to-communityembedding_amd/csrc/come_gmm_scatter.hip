@@ -951,6 +951,133 @@ static int launch_cov_reduce(const float *part, float *out, int64_t n, int chunk
     return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
 }
 
+// ---- M-step parameters + E-step constants (come_gmm_params) ----------------------------------
+//
+// One workgroup per component, float64 in LDS (d <= 128: 128 x 129 doubles = 129 KB): cov =
+// S / nk + reg I (sklearn _estimate_gaussian_covariances_full), the right-looking Cholesky
+// factorisation in place (L in the lower triangle), then X = L^-1 column by column -- one thread
+// per column, no barrier: a column's forward substitution reads only L and its own earlier values,
+// stored transposed in the upper triangle, which is prec_chol = L^-T (sklearn
+// _compute_precision_cholesky: solve_triangular(L, I).T).  Then the E-step's fp32 inputs.  Replaces
+// ~30 small launches (torch cholesky_ex / solve_triangular / einsum) and a host sync per EM
+// iteration.
+struct ParamsArgs {
+    const double *S, *nk, *means, *weights;
+    int K, d;
+    double reg;
+    double *cov, *pc;
+    float *e_pc, *e_mp, *e_ln;
+    int *info;
+};
+
+__global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
+    extern __shared__ __attribute__((aligned(16))) double A[];  // [d][d + 1]
+    __shared__ double ld[128], pd[128], red[256];
+    __shared__ int bad;
+    const int k = blockIdx.x, d = p.d, LD = d + 1, tid = threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+    const double *S = p.S + (int64_t)k * d * d;
+    double *cov = p.cov + (int64_t)k * d * d;
+    for (int i = ty; i < d; i += 16)
+        for (int j = tx; j < d; j += 16) {
+            double v = S[i * d + j] / p.nk[k];  // (the torch path's S / nk[:, None, None], + reg I)
+            if (i == j) v += p.reg;
+            cov[i * d + j] = v;
+            A[i * LD + j] = v;
+        }
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    // Cholesky, right-looking, one barrier per column: step j reads column j below the diagonal
+    // (unscaled) and writes L's column j transposed into row j's upper part (U = L^T) and the
+    // trailing lower triangle -- disjoint, so the scaling and the update share the phase
+    for (int j = 0; j < d; ++j) {
+        const double ajj = A[j * LD + j];
+        const bool ok = ajj > 0.0;
+        const double ljj = sqrt(ok ? ajj : 1.0), rajj = 1.0 / (ok ? ajj : 1.0);
+        if (tid == 0) {
+            ld[j] = ljj;
+            if (!ok && bad == 0) bad = j + 1;
+        }
+        for (int i = j + 1 + tid; i < d; i += 256) A[j * LD + i] = A[i * LD + j] / ljj;
+        // the thread's columns cc = j + 1 + tx + 16 n of column j in registers, then each row's
+        // elements loaded, updated and stored as a batch (loads issue back to back)
+        double cj[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int cc = j + 1 + tx + 16 * n;
+            cj[n] = cc < d ? A[cc * LD + j] : 0.0;
+        }
+        for (int ii = j + 1 + ty; ii < d; ii += 16) {
+            const double t = A[ii * LD + j] * rajj;
+            double v[8];
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const int cc = j + 1 + tx + 16 * n;
+                v[n] = cc <= ii ? A[ii * LD + cc] : 0.0;
+            }
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const int cc = j + 1 + tx + 16 * n;
+                if (cc <= ii) A[ii * LD + cc] = v[n] - t * cj[n];
+            }
+        }
+        __syncthreads();
+    }
+    // P = U^-1 = L^-T (upper), bottom-up by rows: P[r][c] = -(sum_{r<q<=c} U[r][q] P[q][c]) /
+    // U[r][r] for every c > r at once; P[q][c] (q < c) kept in the lower triangle at A[c][q], its
+    // diagonal in pd.  Two threads per column c split the dot by the parity of q, four partial
+    // sums each.
+    for (int r = tid; r < d; r += 256) pd[r] = 1.0 / ld[r];
+    __syncthreads();
+    for (int r = d - 2; r >= 0; --r) {
+        const int c = r + 1 + (tid & 127), h = tid >> 7;
+        double part = 0.0;
+        if (c < d) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            int q = r + 1 + h;
+            for (; q + 6 < c; q += 8) {
+                s0 += A[r * LD + q] * A[c * LD + q];
+                s1 += A[r * LD + q + 2] * A[c * LD + q + 2];
+                s2 += A[r * LD + q + 4] * A[c * LD + q + 4];
+                s3 += A[r * LD + q + 6] * A[c * LD + q + 6];
+            }
+            for (; q <= c; q += 2) s0 += A[r * LD + q] * (q == c ? pd[c] : A[c * LD + q]);
+            part = (s0 + s1) + (s2 + s3);
+        }
+        red[tid] = part;
+        __syncthreads();
+        if (h == 0 && c < d) A[c * LD + r] = -(red[tid] + red[tid + 128]) * pd[r];
+        __syncthreads();
+    }
+    // prec_chol (upper): row r, column c > r at A[c][r], pd on the diagonal
+    double *pc = p.pc + (int64_t)k * d * d;
+    float *epc = p.e_pc + (int64_t)k * d * d;
+    for (int r = ty; r < d; r += 16)
+        for (int c = tx; c < d; c += 16) {
+            const double v = c < r ? 0.0 : (c == r ? pd[r] : A[c * LD + r]);
+            pc[r * d + c] = v;
+            epc[r * d + c] = (float)v;
+        }
+    // mu_k prec_chol_k (column j: rows i <= j) and log det = sum log diag(prec_chol)
+    if (tid < d) {
+        const int j = tid;
+        const double *mu = p.means + (int64_t)k * d;
+        double s = mu[j] * pd[j];
+        for (int i = 0; i < j; ++i) s += mu[i] * A[j * LD + i];
+        p.e_mp[(int64_t)k * d + j] = (float)s;
+    }
+    red[tid] = tid < d ? log(pd[tid]) : 0.0;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) red[tid] += red[tid + w];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        p.e_ln[k] = (float)(log(p.weights[k]) + red[0] - 0.5 * d * log(2.0 * 3.14159265358979323846));
+        p.info[k] = bad;
+    }
+}
+
 }  // namespace come
 
 using namespace come;
@@ -1035,4 +1162,35 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     rc = hip_error(hipGetLastError(), "k_gmm_cov launch");
     if (rc || used == 1) return rc;
     return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
+}
+
+extern "C" int come_gmm_params(const double *scatter, const double *nk, const double *means,
+                               const double *weights, int K, int d, double reg_covar,
+                               double *cov_out, double *prec_chol_out, float *e_prec_chol,
+                               float *e_mu_prec, float *e_log_norm, int *info, void *stream) {
+    if (K < 1 || d < 1 || d > 128)
+        return set_error(COME_E_INVALID, "gmm_params: need K >= 1 and 1 <= d <= 128");
+    if (!scatter || !nk || !means || !weights || !cov_out || !prec_chol_out || !e_prec_chol ||
+        !e_mu_prec || !e_log_norm || !info)
+        return set_error(COME_E_INVALID, "null pointer");
+    int dev;
+    int rc = ensure_init(&dev);
+    if (rc) return rc;
+    static bool attr = false;
+    if (!attr) {
+        // (the kernel's static LDS, ~3 KB, counts against the 160 KB too: ask for what d = 128
+        // needs, 129 KB, not the whole of it -- a refused attribute would also leave an error
+        // for the launch check below to report)
+        rc = hip_error(hipFuncSetAttribute((const void *)k_gmm_params,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(sizeof(double) * 128 * 129)),
+                       "k_gmm_params attribute");
+        if (rc) return rc;
+        attr = true;
+    }
+    ParamsArgs p{scatter, nk, means, weights, K, d, reg_covar, cov_out, prec_chol_out,
+                 e_prec_chol, e_mu_prec, e_log_norm, info};
+    hipLaunchKernelGGL(k_gmm_params, dim3(K), dim3(256), sizeof(double) * (size_t)d * (d + 1),
+                       (hipStream_t)stream, p);
+    return hip_error(hipGetLastError(), "k_gmm_params launch");
 }

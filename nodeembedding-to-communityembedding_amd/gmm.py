@@ -143,6 +143,26 @@ def scatter(X, resp, means, chunks=None):
     return out
 
 
+def params(S, nk, means, weights, reg_covar):
+    """come_gmm_params on device float64 scatter matrices [K, d, d] (d <= 128), nk [K], means
+    [K, d], weights [K]: (cov, prec_chol, e_prec_chol, e_mu_prec, e_log_norm, info), the last
+    four the E-step's fp32 inputs and a device int32 [K] Cholesky status (0 = fine)."""
+    import torch
+    K, d = means.shape
+    dev = S.device
+    cov = torch.empty((K, d, d), dtype=torch.float64, device=dev)
+    pc = torch.empty((K, d, d), dtype=torch.float64, device=dev)
+    e_pc = torch.empty((K, d, d), dtype=torch.float32, device=dev)
+    e_mp = torch.empty((K, d), dtype=torch.float32, device=dev)
+    e_ln = torch.empty((K,), dtype=torch.float32, device=dev)
+    info = torch.empty((K,), dtype=torch.int32, device=dev)
+    check(_lib.lib().come_gmm_params(ptr(S), ptr(nk), ptr(means), ptr(weights), K, d,
+                                     float(reg_covar), ptr(cov), ptr(pc), ptr(e_pc), ptr(e_mp),
+                                     ptr(e_ln), ptr(info), stream_handle(dev)),
+          "come_gmm_params")
+    return cov, pc, e_pc, e_mp, e_ln, info
+
+
 class GaussianMixture(object):
     def __init__(self, n_components=1, covariance_type='full', tol=1e-3, reg_covar=1e-6,
                  max_iter=100, n_init=1, init_params='kmeans', weights_init=None,
@@ -203,6 +223,42 @@ class GaussianMixture(object):
         cov = S / nk[:, None, None]
         cov += self.reg_covar * torch.eye(d, dtype=torch.float64, device=X.device)
         return nk / (self._n_total if world > 1 else V), means, cov
+
+    def _m_step_params(self, X, resp):
+        """One M-step and the E-step inputs it implies: _m_step + _set_params with everything
+        after the scatter in one launch (come_gmm_params: cov, Cholesky, prec_chol = L^-T and the
+        E-step constants in float64, one workgroup per component), for d <= 128.  Returns a
+        device int32 [K] info tensor (non-zero: that component's covariance is not positive
+        definite) for the caller to check with its next host read -- no sync here."""
+        import torch
+        V, d = X.shape
+        K = resp.shape[1]
+        if d > 128:
+            self._set_params(*self._m_step(X, resp))
+            return torch.zeros(K, dtype=torch.int32, device=X.device)
+        world = self._rank_world()[1]
+        nk = resp_sum(resp)
+        sx = resp_t_x(resp, X)
+        if world > 1:
+            all_reduce_sum([nk, sx], self.group)
+        nk = (nk + 10 * np.finfo(np.float64).eps).contiguous()
+        means = (sx / nk[:, None]).contiguous()
+        S = scatter(X, resp, means.float()).double()
+        if world > 1:
+            all_reduce_sum([S], self.group)
+        S = S.contiguous()
+        weights = (nk / (self._n_total if world > 1 else V)).contiguous()
+        cov, pc, e_pc, e_mp, e_ln, info = params(S, nk, means, weights, self.reg_covar)
+        self._w, self._mu, self._cov, self._pc = weights, means, cov, pc
+        self._e_pc, self._e_mp, self._e_ln = e_pc, e_mp, e_ln
+        return info
+
+    @staticmethod
+    def _raise_ill_defined():
+        raise ValueError("Fitting the mixture model failed because some components have "
+                         "ill-defined empirical covariance (for instance caused by "
+                         "singleton or collapsed samples). Try to decrease the number of "
+                         "components, or increase reg_covar.")
 
     def _set_params(self, weights, means, cov):
         import torch
@@ -366,9 +422,12 @@ class GaussianMixture(object):
             for n_iter in range(1, self.max_iter + 1):
                 prev = lb
                 resp, lse = estep(X, self._e_pc, self._e_mp, self._e_ln)
-                w, mu, cov = self._m_step(X, resp)
-                self._set_params(w, mu, cov)
-                lb = self._global_sum(lse.double().sum(), X.device) / self._n_total
+                info = self._m_step_params(X, resp)
+                # one host read per iteration: the lower bound and the Cholesky status together
+                lb_info = torch.stack([lse.double().sum(), (info != 0).any().double()]).cpu()
+                if lb_info[1] != 0:
+                    self._raise_ill_defined()
+                lb = self._global_sum(float(lb_info[0]), X.device) / self._n_total
                 if abs(lb - prev) < self.tol:
                     converged = True
                     break

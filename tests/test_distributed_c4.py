@@ -42,6 +42,19 @@ def _cpu_scatter(X, resp, means, chunks=None):
     return torch.einsum("vk,vkd,vke->kde", resp.double(), Xc, Xc).float()
 
 
+def _cpu_params(S, nk, means, weights, reg):
+    import math
+    d = S.shape[-1]
+    cov = S / nk[:, None, None] + reg * torch.eye(d, dtype=torch.float64)
+    chol, info = torch.linalg.cholesky_ex(cov)
+    eye = torch.eye(d, dtype=torch.float64).expand_as(cov)
+    pc = torch.linalg.solve_triangular(chol, eye, upper=False).transpose(-1, -2).contiguous()
+    log_det = torch.log(torch.diagonal(pc, dim1=-2, dim2=-1)).sum(-1)
+    e_mp = torch.einsum("kd,kde->ke", means, pc).float()
+    e_ln = (torch.log(weights) + log_det - 0.5 * d * math.log(2 * math.pi)).float()
+    return cov, pc, pc.float(), e_mp, e_ln, info.int()
+
+
 def _cpu_community_grad(x, pi, mu, inv, beta, lr, iters):
     x.copy_(torch.from_numpy(orc.community_train(x.numpy(), pi.numpy(), mu.numpy(), inv.numpy(),
                                                  beta, lr, iters)))
@@ -54,6 +67,7 @@ def _cpu_gmm_resp(x, pc, mp_, ln):
 def _patch(setattr_=setattr):
     setattr_(gmm, "estep", _cpu_estep)
     setattr_(gmm, "scatter", _cpu_scatter)
+    setattr_(gmm, "params", _cpu_params)
     setattr_(gmm.GaussianMixture, "_prepare_x",
              lambda self, X: torch.as_tensor(X, dtype=torch.float32).contiguous())
     setattr_(ce, "community_grad", _cpu_community_grad)

@@ -336,3 +336,96 @@ def test_estep_upper_factors_vs_float64(V, K, d, r16):
     ref_lse = logsumexp(lp, 1)
     np.testing.assert_allclose(resp.cpu().numpy(), np.exp(lp - ref_lse[:, None]), atol=2e-4)
     np.testing.assert_allclose(lse.cpu().numpy(), ref_lse, rtol=2e-5, atol=2e-3)
+
+
+def _torch_params(S, nk, means, weights, reg):
+    """The unfused path (GaussianMixture._m_step / _set_params / _prepare_estep): float64 cov,
+    torch Cholesky, prec_chol = solve_triangular(L, I).T, the E-step constants."""
+    import math
+    d = S.shape[-1]
+    cov = S / nk[:, None, None]
+    cov += reg * torch.eye(d, dtype=torch.float64, device=S.device)
+    chol, info = torch.linalg.cholesky_ex(cov)
+    eye = torch.eye(d, dtype=torch.float64, device=S.device).expand_as(cov)
+    pc = torch.linalg.solve_triangular(chol, eye, upper=False).transpose(-1, -2)
+    log_det = torch.log(torch.diagonal(pc, dim1=-2, dim2=-1)).sum(-1)
+    e_mp = torch.einsum("kd,kde->ke", means, pc)
+    e_ln = torch.log(weights) + log_det - 0.5 * d * math.log(2 * math.pi)
+    return cov, pc, e_mp, e_ln, info
+
+
+@pytest.mark.parametrize("K,d", [(50, 128), (3, 64), (5, 17), (1, 128), (7, 100), (2, 1)])
+def test_gmm_params_fused_matches_unfused(K, d):
+    """come_gmm_params (one workgroup per component: cov = S / nk + reg I, in-LDS Cholesky,
+    prec_chol = L^-T by per-column forward substitution, the E-step's constants) against torch's
+    Cholesky / triangular solve in float64: cov bit-identical (the same two operations), prec_chol
+    and the constants to 1e-10 relative (another summation order), the fp32 copies to one
+    rounding.  The scatter inputs are Gram matrices of a few hundred samples (condition numbers
+    up to ~1e3)."""
+    from come_amd import _lib
+    from come_amd._lib import ptr, stream_handle
+    dev = torch.device("cuda", 0)
+    rng = np.random.RandomState(K * 1000 + d)
+    n = 3 * d + 20
+    Y = rng.standard_normal((K, n, d)) * rng.uniform(0.5, 2.0, (K, 1, d))
+    nk = rng.uniform(50.0, 500.0, K)
+    S = np.einsum("kni,knj->kij", Y, Y) * (nk[:, None, None] / n)
+    means = rng.standard_normal((K, d))
+    weights = rng.dirichlet(np.ones(K))
+    reg = 1e-5
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    S_, nk_, mu_, w_ = t(S), t(nk), t(means), t(weights)
+    cov = torch.empty((K, d, d), dtype=torch.float64, device=dev)
+    pc = torch.empty_like(cov)
+    e_pc = torch.empty((K, d, d), dtype=torch.float32, device=dev)
+    e_mp = torch.empty((K, d), dtype=torch.float32, device=dev)
+    e_ln = torch.empty((K,), dtype=torch.float32, device=dev)
+    info = torch.full((K,), -1, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().come_gmm_params(ptr(S_), ptr(nk_), ptr(mu_), ptr(w_), K, d, reg,
+                                          ptr(cov), ptr(pc), ptr(e_pc), ptr(e_mp), ptr(e_ln),
+                                          ptr(info), stream_handle(dev)), "come_gmm_params")
+    rcov, rpc, remp, reln, rinfo = _torch_params(S_, nk_, mu_, w_, reg)
+    assert int(rinfo.abs().sum()) == 0 and info.cpu().numpy().tolist() == [0] * K
+    assert torch.equal(cov, rcov)
+    assert torch.equal(torch.tril(pc, -1), torch.zeros_like(pc))
+    np.testing.assert_allclose(pc.cpu().numpy(), rpc.cpu().numpy(), rtol=1e-10,
+                               atol=1e-10 * float(rpc.abs().max()))
+    np.testing.assert_allclose(e_pc.cpu().numpy(), rpc.float().cpu().numpy(), rtol=1e-6,
+                               atol=1e-6 * float(rpc.abs().max()))
+    np.testing.assert_allclose(e_mp.cpu().numpy(), remp.float().cpu().numpy(), rtol=1e-5,
+                               atol=1e-5 * float(remp.abs().max()))
+    np.testing.assert_allclose(e_ln.cpu().numpy(), reln.float().cpu().numpy(), rtol=1e-6)
+
+
+def test_gmm_params_reports_a_non_positive_pivot():
+    """A component whose covariance is not positive definite (here: a negative eigenvalue past
+    reg_covar) sets info[k] = (first bad pivot) + 1 and leaves the others 0; fit() raises
+    sklearn's ValueError from it (GaussianMixture._raise_ill_defined)."""
+    from come_amd import _lib
+    from come_amd._lib import ptr, stream_handle
+    dev = torch.device("cuda", 0)
+    K, d = 3, 8
+    S = np.stack([np.eye(d) * 2.0] * K)
+    S[1, 3, 3] = -1.0
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    outs = [torch.empty((K, d, d), dtype=torch.float64, device=dev) for _ in range(2)]
+    e_pc = torch.empty((K, d, d), dtype=torch.float32, device=dev)
+    e_mp = torch.empty((K, d), dtype=torch.float32, device=dev)
+    e_ln = torch.empty((K,), dtype=torch.float32, device=dev)
+    info = torch.full((K,), -1, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().come_gmm_params(ptr(t(S)), ptr(t(np.ones(K))), ptr(t(np.zeros((K, d)))),
+                                          ptr(t(np.full(K, 1.0 / K))), K, d, 1e-6, ptr(outs[0]),
+                                          ptr(outs[1]), ptr(e_pc), ptr(e_mp), ptr(e_ln),
+                                          ptr(info), stream_handle(dev)), "come_gmm_params")
+    assert info.cpu().numpy().tolist() == [0, 4, 0]
+    with pytest.raises(_lib.ComeError, match="gmm_params"):
+        _lib.check(_lib.lib().come_gmm_params(ptr(t(S)), ptr(t(np.ones(K))), ptr(t(np.zeros((K, d)))),
+                                              ptr(t(np.ones(K))), K, 129, 1e-6, ptr(outs[0]),
+                                              ptr(outs[1]), ptr(e_pc), ptr(e_mp), ptr(e_ln),
+                                              ptr(info), stream_handle(dev)), "come_gmm_params")
+    # collapsed samples (every row equal, reg_covar 0): zero covariances, sklearn's ValueError
+    with pytest.raises(ValueError, match="ill-defined"):
+        gmm.GaussianMixture(2, reg_covar=0.0, max_iter=3, init_params="random",
+                            random_state=0).fit(torch.as_tensor(np.zeros((40, 8), np.float32) +
+                                                                np.arange(8, dtype=np.float32),
+                                                                device=dev))
