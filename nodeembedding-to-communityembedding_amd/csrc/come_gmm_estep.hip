@@ -489,6 +489,26 @@ __device__ __forceinline__ float r16t_lp_of(float sq, const float *par) {
 }
 
 // online log-sum-exp step
+// A row's responsibilities from its stored log-probabilities: the row's four lanes (group kg)
+// take components k = kg, kg + 4, ..., each lane's loads issued as a batch of up to 16 before any
+// exp or store (one memory round trip where one lane walking all K took K); the last component's
+// value comes from the register that would have stored it.
+__device__ __forceinline__ void resp_normalize(float *lp, int K, float lp_last, float lse, int kg) {
+    for (int k0 = kg; k0 < K; k0 += 64) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int k = k0 + 4 * u;
+            v[u] = k < K - 1 ? lp[k] : lp_last;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int k = k0 + 4 * u;
+            if (k < K) lp[k] = expf(v[u] - lse);
+        }
+    }
+}
+
 __device__ __forceinline__ void lse_push(float lp, float &run_max, float &run_sum) {
     if (lp > run_max) {
         run_sum = run_sum * expf(run_max - lp) + 1.0f;
@@ -744,12 +764,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
         lse_push(lp, run_max, run_sum);
         lp_prev = lp;
     }
-    if (owner) {
-        float *lp = a.resp + row * a.K;
-        lp[a.K - 1] = lp_prev;
+    if (rowok) {  // the row's four lanes (the reduction left the sums in all of them)
         const float lse = run_max + logf(run_sum);
-        for (int k = 0; k < a.K; ++k) lp[k] = expf(lp[k] - lse);
-        if (a.lse) a.lse[row] = lse;
+        resp_normalize(a.resp + row * a.K, a.K, lp_prev, lse, kg);
+        if (a.lse && kg == 0) a.lse[row] = lse;
     }
 }
 
