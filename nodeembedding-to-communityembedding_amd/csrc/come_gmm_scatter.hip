@@ -31,6 +31,8 @@ struct CovArgs {
     int64_t rows_per_chunk;
     int d;
     int K;
+    int upper_only;  // 32-wide-tile kernels writing chunk partials: only the upper tiles (the
+                     // reduction mirrors them), no transposed (uncoalesced) stores
 };
 
 // ---- M-step scatter on v_mfma_f32_16x16x4_f32 (k_gmm_cov16, gmm_cov_async = 3) ----------------
@@ -494,7 +496,7 @@ __device__ __forceinline__ void covbf3_part(const CovArgs &a, const char *smb, i
         for (int r = 0; r < 16; ++r) {
             const int ii = 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
             out[(int64_t)ii * D + jj] = acc[n][r];
-            if (ta != tb) out[(int64_t)jj * D + ii] = acc[n][r];
+            if (ta != tb && !a.upper_only) out[(int64_t)jj * D + ii] = acc[n][r];
         }
     }
 }
@@ -798,7 +800,7 @@ __device__ __forceinline__ void covfb3_body(const CovArgs &a, char *smb, int nb,
         for (int r = 0; r < 16; ++r) {
             const int ii = 32 * ta + (r & 3) + 8 * (r >> 2) + 4 * h;
             out[(int64_t)ii * D + jj] = acc[n][r];
-            if (ta != tb) out[(int64_t)jj * D + ii] = acc[n][r];
+            if (ta != tb && !a.upper_only) out[(int64_t)jj * D + ii] = acc[n][r];
         }
     }
 }
@@ -939,6 +941,37 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float
     }
 }
 
+// The 32-wide-tile kernels' partials hold only the upper tiles (CovArgs::upper_only): thread q
+// sums entries 4 q .. 4 q + 3 of a row of an upper tile over the chunks (16-byte loads, in chunk
+// order) and writes them and their mirror images; lower-tile threads return.
+template <int D>
+__global__ void __launch_bounds__(256) k_gmm_cov_reduce_upper(const float *part, float *out,
+                                                              int64_t n, int chunks) {
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (4 * q >= n) return;
+    const int e = (int)((4 * q) % (D * D)), i = e / D, j = e % D;
+    if ((j >> 5) < (i >> 5)) return;  // a lower tile: the mirror of an upper one
+    const f32x4 *p = reinterpret_cast<const f32x4 *>(part) + q;
+    const int64_t stride = n / 4;
+    f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
+    int c = 0;
+    for (; c + 8 <= chunks; c += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(c + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; c < chunks; ++c) s += p[(int64_t)c * stride];
+    reinterpret_cast<f32x4 *>(out)[q] = s;
+    if ((j >> 5) > (i >> 5)) {
+        float *m = out + (4 * q - e) + (int64_t)j * D + i;  // (j, i) of the same component
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m[(int64_t)t * D] = s[t];
+    }
+}
+
 static int launch_cov_reduce(const float *part, float *out, int64_t n, int chunks,
                              hipStream_t stream) {
     const unsigned grid = (unsigned)((n + 1023) / 1024);
@@ -949,6 +982,18 @@ static int launch_cov_reduce(const float *part, float *out, int64_t n, int chunk
         hipLaunchKernelGGL(k_gmm_cov_reduce<false>, dim3(grid), dim3(256), 0, stream, part, out, n,
                            chunks);
     return hip_error(hipGetLastError(), "k_gmm_cov_reduce launch");
+}
+
+static int launch_cov_reduce_upper(const float *part, float *out, int64_t n, int chunks, int d,
+                                   hipStream_t stream) {
+    const unsigned grid = (unsigned)((n + 1023) / 1024);
+    if (d == 64)
+        hipLaunchKernelGGL(k_gmm_cov_reduce_upper<64>, dim3(grid), dim3(256), 0, stream, part, out,
+                           n, chunks);
+    else
+        hipLaunchKernelGGL(k_gmm_cov_reduce_upper<128>, dim3(grid), dim3(256), 0, stream, part,
+                           out, n, chunks);
+    return hip_error(hipGetLastError(), "k_gmm_cov_reduce_upper launch");
 }
 
 // ---- M-step parameters + E-step constants (come_gmm_params) ----------------------------------
@@ -1098,7 +1143,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
     per = (per + kCovRB - 1) / kCovRB * kCovRB;
     if (per < kCovRB) per = kCovRB;
     const int used = V == 0 ? 1 : (int)((V + per - 1) / per);
-    CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K};
+    CovArgs a{x, resp, means, used > 1 ? scratch : scatter_out, V, per, d, K, 0};
     const bool mfma = (d == 64 || d == 128) && ((uintptr_t)x % 16) == 0;
     if (d > 128) {
         const int nt = (d + 63) / 64;
@@ -1130,11 +1175,13 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr5 = true;
         }
+        a.upper_only = used > 1;
         hipLaunchKernelGGL(k_gmm_cov_fb3<128>, dim3((K + CovFb3<128>::CPW - 1) / CovFb3<128>::CPW, used),
                            dim3(CovFb3<128>::THREADS), CovFb3<128>::LDS_BYTES, (hipStream_t)stream, a);
         rc = hip_error(hipGetLastError(), "k_gmm_cov_fb3 launch");
         if (rc || used == 1) return rc;
-        return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
+        return launch_cov_reduce_upper((const float *)scratch, scatter_out, n, used, d,
+                                       (hipStream_t)stream);
     }
     if (mfma && (cv == 4 || cv == 5)) {
         static bool attr4 = false;
@@ -1145,6 +1192,7 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
             attr4 = true;
         }
         const int cpw = d == 64 ? CovBf3<64>::CPW : CovBf3<128>::CPW;
+        a.upper_only = used > 1;
         hipLaunchKernelGGL(d == 64 ? k_gmm_cov_bf3<64> : k_gmm_cov_bf3<128>,
                            dim3((K + cpw - 1) / cpw, used),
                            dim3(d == 64 ? CovBf3<64>::THREADS : CovBf3<128>::THREADS),
@@ -1152,7 +1200,8 @@ extern "C" int come_gmm_scatter(const float *x, int64_t V, int d, const float *r
                            (hipStream_t)stream, a);
         rc = hip_error(hipGetLastError(), "k_gmm_cov_bf3 launch");
         if (rc || used == 1) return rc;
-        return launch_cov_reduce((const float *)scratch, scatter_out, n, used, (hipStream_t)stream);
+        return launch_cov_reduce_upper((const float *)scratch, scatter_out, n, used, d,
+                                       (hipStream_t)stream);
     }
     void (*kern)(CovArgs) = !mfma ? k_gmm_cov_valu : (d == 64 ? k_gmm_cov16<64> : k_gmm_cov16<128>);
     const int threads = !mfma ? 256 : (d == 64 ? Cov16<64>::THREADS : Cov16<128>::THREADS);
