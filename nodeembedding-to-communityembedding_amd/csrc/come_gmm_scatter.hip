@@ -1000,14 +1000,13 @@ static int launch_cov_reduce_upper(const float *part, float *out, int64_t n, int
 //
 // One workgroup per component, float64 in LDS (d <= 128: 128 x 129 doubles = 129 KB): cov =
 // S / nk + reg I (sklearn _estimate_gaussian_covariances_full), the right-looking Cholesky
-// factorisation in place (L in the lower triangle), then X = L^-1 column by column -- one thread
-// per column, no barrier: a column's forward substitution reads only L and its own earlier values,
-// stored transposed in the upper triangle, which is prec_chol = L^-T (sklearn
-// _compute_precision_cholesky: solve_triangular(L, I).T).  Then the E-step's fp32 inputs.  Replaces
-// ~30 small launches (torch cholesky_ex / solve_triangular / einsum) and a host sync per EM
-// iteration.
+// factorisation in place (U = L^T in the upper triangle), then prec_chol = L^-T = U^-1 bottom-up by
+// rows with two lanes of one wavefront per column (sklearn _compute_precision_cholesky:
+// solve_triangular(L, I).T): a column's values are written and read by its own wavefront only, so
+// the inverse needs no barrier.  Then the E-step's fp32 inputs.  Replaces ~30 small launches (torch
+// cholesky_ex / solve_triangular / einsum) and a host sync per EM iteration.
 struct ParamsArgs {
-    const double *S, *nk, *means, *weights;
+    const double *__restrict__ S, *__restrict__ nk, *__restrict__ means, *__restrict__ weights;
     int K, d;
     double reg;
     double *cov, *pc;
@@ -1017,19 +1016,29 @@ struct ParamsArgs {
 
 __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     extern __shared__ __attribute__((aligned(16))) double A[];  // [d][d + 1]
-    __shared__ double ld[128], pd[128], red[256];
+    __shared__ double ld[128], pd[128], mus[128], red[256];
     __shared__ int bad;
-    const int k = blockIdx.x, d = p.d, LD = d + 1, tid = threadIdx.x;
+    const int k = blockIdx.x, d = p.d, LD = d + 1, tid = threadIdx.x, dd = d * d;
     const int tx = tid & 15, ty = tid >> 4;
-    const double *S = p.S + (int64_t)k * d * d;
-    double *cov = p.cov + (int64_t)k * d * d;
-    for (int i = ty; i < d; i += 16)
-        for (int j = tx; j < d; j += 16) {
-            double v = S[i * d + j] / p.nk[k];  // (the torch path's S / nk[:, None, None], + reg I)
-            if (i == j) v += p.reg;
-            cov[i * d + j] = v;
-            A[i * LD + j] = v;
+    const double *__restrict__ S = p.S + (int64_t)k * dd;
+    double *__restrict__ cov = p.cov + (int64_t)k * dd;
+    const double nkk = p.nk[k];
+    // S / nk[:, None, None] + reg I (the torch path's order), 16 coalesced loads in flight per lane
+    for (int base = tid; base < dd; base += 256 * 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = base + 256 * u < dd ? S[base + 256 * u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = base + 256 * u;
+            if (e >= dd) break;
+            const int i = e / d, j = e - i * d;
+            const double c = i == j ? v[u] / nkk + p.reg : v[u] / nkk;
+            cov[e] = c;
+            A[i * LD + j] = c;
         }
+    }
+    if (tid < d) mus[tid] = p.means[(int64_t)k * d + tid];
     if (tid == 0) bad = 0;
     __syncthreads();
     // Cholesky, right-looking, one barrier per column: step j reads column j below the diagonal
@@ -1069,31 +1078,35 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
         __syncthreads();
     }
     // P = U^-1 = L^-T (upper), bottom-up by rows: P[r][c] = -(sum_{r<q<=c} U[r][q] P[q][c]) /
-    // U[r][r] for every c > r at once; P[q][c] (q < c) kept in the lower triangle at A[c][q], its
-    // diagonal in pd.  Two threads per column c split the dot by the parity of q, four partial
-    // sums each.
+    // U[r][r]; P[q][c] (q < c) kept in the lower triangle at A[c][q], its diagonal in pd.  Column
+    // c = tid / 2 belongs to lanes 2c, 2c + 1 of one wavefront, which split the dot by the parity
+    // of q (four partial sums each) and combine by a lane exchange: every P value a lane reads was
+    // written by its own wavefront at an earlier row (LDS accesses of a wavefront are ordered), so
+    // the rows need no barrier.
     for (int r = tid; r < d; r += 256) pd[r] = 1.0 / ld[r];
     __syncthreads();
-    for (int r = d - 2; r >= 0; --r) {
-        const int c = r + 1 + (tid & 127), h = tid >> 7;
-        double part = 0.0;
-        if (c < d) {
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-            int q = r + 1 + h;
-            for (; q + 6 < c; q += 8) {
-                s0 += A[r * LD + q] * A[c * LD + q];
-                s1 += A[r * LD + q + 2] * A[c * LD + q + 2];
-                s2 += A[r * LD + q + 4] * A[c * LD + q + 4];
-                s3 += A[r * LD + q + 6] * A[c * LD + q + 6];
+    {
+        const int c = tid >> 1, h = tid & 1;
+        const double pdc = c < d ? pd[c] : 0.0;
+        for (int r = d - 2; r >= 0; --r) {
+            double part = 0.0;
+            if (c < d && c > r) {
+                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+                int q = r + 1 + h;
+                for (; q + 6 < c; q += 8) {
+                    s0 += A[r * LD + q] * A[c * LD + q];
+                    s1 += A[r * LD + q + 2] * A[c * LD + q + 2];
+                    s2 += A[r * LD + q + 4] * A[c * LD + q + 4];
+                    s3 += A[r * LD + q + 6] * A[c * LD + q + 6];
+                }
+                for (; q <= c; q += 2) s0 += A[r * LD + q] * (q == c ? pdc : A[c * LD + q]);
+                part = (s0 + s1) + (s2 + s3);
             }
-            for (; q <= c; q += 2) s0 += A[r * LD + q] * (q == c ? pd[c] : A[c * LD + q]);
-            part = (s0 + s1) + (s2 + s3);
+            const double other = __shfl_xor(part, 1);
+            if (h == 0 && c < d && c > r) A[c * LD + r] = -(part + other) * pd[r];
         }
-        red[tid] = part;
-        __syncthreads();
-        if (h == 0 && c < d) A[c * LD + r] = -(red[tid] + red[tid + 128]) * pd[r];
-        __syncthreads();
     }
+    __syncthreads();
     // prec_chol (upper): row r, column c > r at A[c][r], pd on the diagonal
     double *pc = p.pc + (int64_t)k * d * d;
     float *epc = p.e_pc + (int64_t)k * d * d;
@@ -1106,9 +1119,8 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     // mu_k prec_chol_k (column j: rows i <= j) and log det = sum log diag(prec_chol)
     if (tid < d) {
         const int j = tid;
-        const double *mu = p.means + (int64_t)k * d;
-        double s = mu[j] * pd[j];
-        for (int i = 0; i < j; ++i) s += mu[i] * A[j * LD + i];
+        double s = mus[j] * pd[j];
+        for (int i = 0; i < j; ++i) s += mus[i] * A[j * LD + i];
         p.e_mp[(int64_t)k * d + j] = (float)s;
     }
     red[tid] = tid < d ? log(pd[tid]) : 0.0;
