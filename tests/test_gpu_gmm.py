@@ -357,7 +357,7 @@ def _torch_params(S, nk, means, weights, reg):
 @pytest.mark.parametrize("K,d", [(50, 128), (3, 64), (5, 17), (1, 128), (7, 100), (2, 1)])
 def test_gmm_params_fused_matches_unfused(K, d):
     """come_gmm_params (one workgroup per component: cov = S / nk + reg I, in-LDS Cholesky,
-    prec_chol = L^-T by per-column forward substitution, the E-step's constants) against torch's
+    prec_chol = L^-T by rows of back substitution, the E-step's constants) against torch's
     Cholesky / triangular solve in float64: cov bit-identical (the same two operations), prec_chol
     and the constants to 1e-10 relative (another summation order), the fp32 copies to one
     rounding.  The scatter inputs are Gram matrices of a few hundred samples (condition numbers
