@@ -59,8 +59,11 @@ __global__ void __launch_bounds__(kThreads) k_gmm_resp(RespArgs a) {
 __global__ void __launch_bounds__(256) k_gmm_lower_flags(const float *__restrict__ P, int D,
                                                          int *__restrict__ flags, int K) {
     const float *Pk = P + (int64_t)blockIdx.x * D * D;
+    // the strictly lower triangle only, 16 lanes per row segment (no per-element division)
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     int nz = 0;
-    for (int o = threadIdx.x; o < D * D; o += 256) nz |= (o / D > o % D) && Pk[o] != 0.0f;
+    for (int r = 1 + ty; r < D; r += 16)
+        for (int c = tx; c < r; c += 16) nz |= Pk[(int64_t)r * D + c] != 0.0f;
     nz = __syncthreads_or(nz);
     if (threadIdx.x == 0) {
         flags[blockIdx.x] = nz ? 1 : 0;

@@ -1088,7 +1088,44 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     {
         const int c = tid >> 1, h = tid & 1;
         const double pdc = c < d ? pd[c] : 0.0;
-        for (int r = d - 2; r >= 0; --r) {
+        // rows r and r - 1 per round: both dots over q > r share the loads of P[q][c]; then
+        // P[r - 1][c] adds U[r - 1][r] P[r][c] (half the dependent rounds)
+        int r = d - 2;
+        for (; r >= 1; r -= 2) {
+            const int r1 = r - 1;
+            double pa = 0.0, pb = 0.0;
+            if (c < d && c > r) {
+                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+                double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+                int q = r + 1 + h;
+                for (; q + 6 < c; q += 8) {
+                    const double p0 = A[c * LD + q], p1 = A[c * LD + q + 2];
+                    const double p2 = A[c * LD + q + 4], p3 = A[c * LD + q + 6];
+                    a0 += A[r * LD + q] * p0;
+                    a1 += A[r * LD + q + 2] * p1;
+                    a2 += A[r * LD + q + 4] * p2;
+                    a3 += A[r * LD + q + 6] * p3;
+                    b0 += A[r1 * LD + q] * p0;
+                    b1 += A[r1 * LD + q + 2] * p1;
+                    b2 += A[r1 * LD + q + 4] * p2;
+                    b3 += A[r1 * LD + q + 6] * p3;
+                }
+                for (; q <= c; q += 2) {
+                    const double pq = q == c ? pdc : A[c * LD + q];
+                    a0 += A[r * LD + q] * pq;
+                    b0 += A[r1 * LD + q] * pq;
+                }
+                pa = (a0 + a1) + (a2 + a3);
+                pb = (b0 + b1) + (b2 + b3);
+            }
+            const double oa = __shfl_xor(pa, 1), ob = __shfl_xor(pb, 1);
+            if (h == 0 && c < d && c >= r) {
+                const double prc = c > r ? -(pa + oa) * pd[r] : pd[r];  // P[r][c]
+                if (c > r) A[c * LD + r] = prc;
+                A[c * LD + r1] = -(A[r1 * LD + r] * prc + (pb + ob)) * pd[r1];
+            }
+        }
+        if (r == 0) {  // the last row of an even d, alone
             double part = 0.0;
             if (c < d && c > r) {
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
