@@ -1041,39 +1041,64 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     if (tid < d) mus[tid] = p.means[(int64_t)k * d + tid];
     if (tid == 0) bad = 0;
     __syncthreads();
-    // Cholesky, right-looking, one barrier per column: step j reads column j below the diagonal
-    // (unscaled) and writes L's column j transposed into row j's upper part (U = L^T) and the
-    // trailing lower triangle -- disjoint, so the scaling and the update share the phase
-    for (int j = 0; j < d; ++j) {
+    // Cholesky, right-looking, two columns per barrier: steps j and j + 1 = j1 in one phase.  Step
+    // j's update of column j1 is recomputed in registers wherever step j1 needs it (the same
+    // expressions in the same order as one step at a time, so the factor is bit-identical); the
+    // rows j and j1 of U = L^T go to the upper triangle, the trailing update (both steps, per
+    // element) to the lower -- disjoint.
+    int j = 0;
+    for (; j + 1 < d; j += 2) {
+        const int j1 = j + 1;
         const double ajj = A[j * LD + j];
-        const bool ok = ajj > 0.0;
-        const double ljj = sqrt(ok ? ajj : 1.0), rajj = 1.0 / (ok ? ajj : 1.0);
+        const bool ok0 = ajj > 0.0;
+        const double ljj = sqrt(ok0 ? ajj : 1.0), rajj = 1.0 / (ok0 ? ajj : 1.0);
+        const double a10 = A[j1 * LD + j];
+        const double a11 = A[j1 * LD + j1] - (a10 * rajj) * a10;  // step j's update of (j1, j1)
+        const bool ok1 = a11 > 0.0;
+        const double l11 = sqrt(ok1 ? a11 : 1.0), ra11 = 1.0 / (ok1 ? a11 : 1.0);
         if (tid == 0) {
             ld[j] = ljj;
-            if (!ok && bad == 0) bad = j + 1;
+            ld[j1] = l11;
+            if (!ok0 && bad == 0) bad = j + 1;
+            else if (!ok1 && bad == 0) bad = j1 + 1;
         }
-        for (int i = j + 1 + tid; i < d; i += 256) A[j * LD + i] = A[i * LD + j] / ljj;
-        // the thread's columns cc = j + 1 + tx + 16 n of column j in registers, then each row's
-        // elements loaded, updated and stored as a batch (loads issue back to back)
-        double cj[8];
+        for (int i = j1 + tid; i < d; i += 256) {
+            const double ci = A[i * LD + j];
+            A[j * LD + i] = ci / ljj;
+            if (i > j1) A[j1 * LD + i] = (A[i * LD + j1] - (ci * rajj) * a10) / l11;
+        }
+        // the thread's columns cc = j + 2 + tx + 16 n of columns j and j1 (after step j) in
+        // registers, then each row's elements loaded, updated by both steps and stored as a batch
+        double c0[8], c1[8];
 #pragma unroll
         for (int n = 0; n < 8; ++n) {
-            const int cc = j + 1 + tx + 16 * n;
-            cj[n] = cc < d ? A[cc * LD + j] : 0.0;
+            const int cc = j + 2 + tx + 16 * n;
+            c0[n] = cc < d ? A[cc * LD + j] : 0.0;
+            c1[n] = cc < d ? A[cc * LD + j1] - (c0[n] * rajj) * a10 : 0.0;
         }
-        for (int ii = j + 1 + ty; ii < d; ii += 16) {
-            const double t = A[ii * LD + j] * rajj;
+        for (int ii = j + 2 + ty; ii < d; ii += 16) {
+            const double t0 = A[ii * LD + j] * rajj;
+            const double t1 = (A[ii * LD + j1] - t0 * a10) * ra11;
             double v[8];
 #pragma unroll
             for (int n = 0; n < 8; ++n) {
-                const int cc = j + 1 + tx + 16 * n;
+                const int cc = j + 2 + tx + 16 * n;
                 v[n] = cc <= ii ? A[ii * LD + cc] : 0.0;
             }
 #pragma unroll
             for (int n = 0; n < 8; ++n) {
-                const int cc = j + 1 + tx + 16 * n;
-                if (cc <= ii) A[ii * LD + cc] = v[n] - t * cj[n];
+                const int cc = j + 2 + tx + 16 * n;
+                if (cc <= ii) A[ii * LD + cc] = (v[n] - t0 * c0[n]) - t1 * c1[n];
             }
+        }
+        __syncthreads();
+    }
+    if (j < d) {  // an odd d's last column: its pivot only
+        const double ajj = A[j * LD + j];
+        const bool ok = ajj > 0.0;
+        if (tid == 0) {
+            ld[j] = sqrt(ok ? ajj : 1.0);
+            if (!ok && bad == 0) bad = j + 1;
         }
         __syncthreads();
     }
