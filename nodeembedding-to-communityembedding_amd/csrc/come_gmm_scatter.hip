@@ -1014,6 +1014,98 @@ struct ParamsArgs {
     int *info;
 };
 
+// Right-looking Cholesky steps j .. j + NB - 1 in one phase (no barrier inside).  Step m turns
+// A^(m) into A^(m+1)[i][c] = A^(m)[i][c] - t_m(i) A^(m)[c][j + m], t_m(i) = A^(m)[i][j + m] / pivot_m.
+// Each thread recomputes, in registers and in exactly that order, the panel values A^(m)[i][j + m]
+// it needs (the same expressions as one step per barrier, so the factor is bit-identical), writes
+// rows j + m of U = L^T to the upper triangle and the NB steps' trailing update to the lower --
+// disjoint from every read of the phase.
+template <int NB>
+__device__ __forceinline__ void chol_panel(double *A, int LD, int d, int j, int tid, double *ld,
+                                           int *bad) {
+    const int tx = tid & 15, ty = tid >> 4;
+    double P[NB][NB], ra[NB], lk[NB];  // P[k][m] = A^(m)[j + k][j + m], m < k
+    bool okv[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        double t[NB];
+#pragma unroll
+        for (int m = 0; m <= k; ++m) {
+            double x = A[(j + k) * LD + j + m];
+#pragma unroll
+            for (int q = 0; q < m; ++q) x = x - t[q] * P[m][q];
+            if (m < k) {
+                P[k][m] = x;
+                t[m] = x * ra[m];
+            } else {
+                okv[k] = x > 0.0;
+                lk[k] = sqrt(okv[k] ? x : 1.0);
+                ra[k] = 1.0 / (okv[k] ? x : 1.0);
+            }
+        }
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            ld[j + k] = lk[k];
+            if (!okv[k] && *bad == 0) *bad = j + k + 1;
+        }
+    }
+    // U rows j + m: U[j + m][i] = A^(m)[i][j + m] / L[j + m][j + m] for i > j + m
+    for (int i = j + 1 + tid; i < d; i += 256) {
+        double t[NB];
+#pragma unroll
+        for (int m = 0; m < NB; ++m) {
+            if (j + m >= i) break;
+            double x = A[i * LD + j + m];
+#pragma unroll
+            for (int q = 0; q < m; ++q) x = x - t[q] * P[m][q];
+            t[m] = x * ra[m];
+            A[(j + m) * LD + i] = x / lk[m];
+        }
+    }
+    // trailing rows / columns from j + NB: the thread's columns cc = j + NB + tx + 16 n with their
+    // panel values in registers, then each row's elements loaded, updated by the NB steps, stored
+    double c[NB][8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+        const int cc = j + NB + tx + 16 * n;
+        double t[NB];
+#pragma unroll
+        for (int m = 0; m < NB; ++m) {
+            double x = cc < d ? A[cc * LD + j + m] : 0.0;
+#pragma unroll
+            for (int q = 0; q < m; ++q) x = x - t[q] * P[m][q];
+            t[m] = x * ra[m];
+            c[m][n] = x;
+        }
+    }
+    for (int ii = j + NB + ty; ii < d; ii += 16) {
+        double t[NB];
+#pragma unroll
+        for (int m = 0; m < NB; ++m) {
+            double x = A[ii * LD + j + m];
+#pragma unroll
+            for (int q = 0; q < m; ++q) x = x - t[q] * P[m][q];
+            t[m] = x * ra[m];
+        }
+        double v[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int cc = j + NB + tx + 16 * n;
+            v[n] = cc <= ii ? A[ii * LD + cc] : 0.0;
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int cc = j + NB + tx + 16 * n;
+            double y = v[n];
+#pragma unroll
+            for (int m = 0; m < NB; ++m) y = y - t[m] * c[m][n];
+            if (cc <= ii) A[ii * LD + cc] = y;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     extern __shared__ __attribute__((aligned(16))) double A[];  // [d][d + 1]
     __shared__ double ld[128], pd[128], mus[128], red[256];
@@ -1041,65 +1133,19 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     if (tid < d) mus[tid] = p.means[(int64_t)k * d + tid];
     if (tid == 0) bad = 0;
     __syncthreads();
-    // Cholesky, right-looking, two columns per barrier: steps j and j + 1 = j1 in one phase.  Step
-    // j's update of column j1 is recomputed in registers wherever step j1 needs it (the same
-    // expressions in the same order as one step at a time, so the factor is bit-identical); the
-    // rows j and j1 of U = L^T go to the upper triangle, the trailing update (both steps, per
-    // element) to the lower -- disjoint.
+    // Cholesky, right-looking, four columns per barrier (chol_panel)
     int j = 0;
-    for (; j + 1 < d; j += 2) {
-        const int j1 = j + 1;
-        const double ajj = A[j * LD + j];
-        const bool ok0 = ajj > 0.0;
-        const double ljj = sqrt(ok0 ? ajj : 1.0), rajj = 1.0 / (ok0 ? ajj : 1.0);
-        const double a10 = A[j1 * LD + j];
-        const double a11 = A[j1 * LD + j1] - (a10 * rajj) * a10;  // step j's update of (j1, j1)
-        const bool ok1 = a11 > 0.0;
-        const double l11 = sqrt(ok1 ? a11 : 1.0), ra11 = 1.0 / (ok1 ? a11 : 1.0);
-        if (tid == 0) {
-            ld[j] = ljj;
-            ld[j1] = l11;
-            if (!ok0 && bad == 0) bad = j + 1;
-            else if (!ok1 && bad == 0) bad = j1 + 1;
-        }
-        for (int i = j1 + tid; i < d; i += 256) {
-            const double ci = A[i * LD + j];
-            A[j * LD + i] = ci / ljj;
-            if (i > j1) A[j1 * LD + i] = (A[i * LD + j1] - (ci * rajj) * a10) / l11;
-        }
-        // the thread's columns cc = j + 2 + tx + 16 n of columns j and j1 (after step j) in
-        // registers, then each row's elements loaded, updated by both steps and stored as a batch
-        double c0[8], c1[8];
-#pragma unroll
-        for (int n = 0; n < 8; ++n) {
-            const int cc = j + 2 + tx + 16 * n;
-            c0[n] = cc < d ? A[cc * LD + j] : 0.0;
-            c1[n] = cc < d ? A[cc * LD + j1] - (c0[n] * rajj) * a10 : 0.0;
-        }
-        for (int ii = j + 2 + ty; ii < d; ii += 16) {
-            const double t0 = A[ii * LD + j] * rajj;
-            const double t1 = (A[ii * LD + j1] - t0 * a10) * ra11;
-            double v[8];
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                const int cc = j + 2 + tx + 16 * n;
-                v[n] = cc <= ii ? A[ii * LD + cc] : 0.0;
-            }
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                const int cc = j + 2 + tx + 16 * n;
-                if (cc <= ii) A[ii * LD + cc] = (v[n] - t0 * c0[n]) - t1 * c1[n];
-            }
-        }
+    for (; j + 4 <= d; j += 4) {
+        chol_panel<4>(A, LD, d, j, tid, ld, &bad);
         __syncthreads();
     }
-    if (j < d) {  // an odd d's last column: its pivot only
-        const double ajj = A[j * LD + j];
-        const bool ok = ajj > 0.0;
-        if (tid == 0) {
-            ld[j] = sqrt(ok ? ajj : 1.0);
-            if (!ok && bad == 0) bad = j + 1;
-        }
+    if (j + 2 <= d) {
+        chol_panel<2>(A, LD, d, j, tid, ld, &bad);
+        __syncthreads();
+        j += 2;
+    }
+    if (j < d) {
+        chol_panel<1>(A, LD, d, j, tid, ld, &bad);
         __syncthreads();
     }
     // P = U^-1 = L^-T (upper), bottom-up by rows: P[r][c] = -(sum_{r<q<=c} U[r][q] P[q][c]) /
