@@ -1106,6 +1106,72 @@ __device__ __forceinline__ void chol_panel(double *A, int LD, int d, int j, int 
     }
 }
 
+// Rows r, r - 1, .., r - R + 1 of P = U^-1 for the lane pair of column c (h: the parity of q it
+// sums): the R dots over q > r share the loads of P[q][c]; then row r - k adds U[r - k][q] P[q][c]
+// for q = r, r - 1, .., r - k + 1 from registers before its dot.  P[q][c] (q < c) sits at A[c][q],
+// the diagonal in pd.  Written by the h = 0 lane; read back only by this wavefront.
+template <int R>
+__device__ __forceinline__ void inv_rows(double *A, int LD, int d, int r, int c, int h,
+                                         double pdc, const double *pd) {
+    double S[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) S[k] = 0.0;
+    if (c < d && c > r) {
+        double s[R][4];
+#pragma unroll
+        for (int k = 0; k < R; ++k) s[k][0] = s[k][1] = s[k][2] = s[k][3] = 0.0;
+        int q = r + 1 + h;
+        for (; q + 6 < c; q += 8) {
+            const double p0 = A[c * LD + q], p1 = A[c * LD + q + 2];
+            const double p2 = A[c * LD + q + 4], p3 = A[c * LD + q + 6];
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const double *u = A + (r - k) * LD + q;
+                s[k][0] += u[0] * p0;
+                s[k][1] += u[2] * p1;
+                s[k][2] += u[4] * p2;
+                s[k][3] += u[6] * p3;
+            }
+        }
+        for (; q <= c; q += 2) {
+            const double pq = q == c ? pdc : A[c * LD + q];
+#pragma unroll
+            for (int k = 0; k < R; ++k) s[k][0] += A[(r - k) * LD + q] * pq;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) S[k] = (s[k][0] + s[k][1]) + (s[k][2] + s[k][3]);
+    }
+    double O[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) O[k] = __shfl_xor(S[k], 1);
+    if (h == 0 && c < d && c >= r - R + 1) {
+        double Pv[R];  // P[r - k][c]
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int rk = r - k;
+            if (c <= rk) {
+                Pv[k] = c == rk ? pd[rk] : 0.0;
+                continue;
+            }
+            double acc;
+            if (k == 0) {
+                acc = S[0] + O[0];
+            } else {
+                acc = A[rk * LD + r] * Pv[0];
+#pragma unroll
+                for (int m = 1; m < k; ++m) acc = acc + A[rk * LD + r - m] * Pv[m];
+                acc = acc + (S[k] + O[k]);
+            }
+            Pv[k] = -acc * pd[rk];
+            A[c * LD + rk] = Pv[k];
+        }
+    }
+}
+
+// Cholesky columns per barrier and inverse rows per round (scripts/params_ab.py at K = 50, d = 128:
+// 8 / 4 -> 0.190 ms, 4 / 4 0.198, 8 / 2 0.215, 4 / 2 0.223; profiles/r07_ab_gmm_params6.txt)
+constexpr int kParamsNB = 8, kParamsInvR = 4;
+
 __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     extern __shared__ __attribute__((aligned(16))) double A[];  // [d][d + 1]
     __shared__ double ld[128], pd[128], mus[128], red[256];
@@ -1135,9 +1201,14 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     __syncthreads();
     // Cholesky, right-looking, four columns per barrier (chol_panel)
     int j = 0;
-    for (; j + 4 <= d; j += 4) {
+    for (; j + kParamsNB <= d; j += kParamsNB) {
+        chol_panel<kParamsNB>(A, LD, d, j, tid, ld, &bad);
+        __syncthreads();
+    }
+    if (kParamsNB > 4 && j + 4 <= d) {
         chol_panel<4>(A, LD, d, j, tid, ld, &bad);
         __syncthreads();
+        j += 4;
     }
     if (j + 2 <= d) {
         chol_panel<2>(A, LD, d, j, tid, ld, &bad);
@@ -1159,60 +1230,14 @@ __global__ void __launch_bounds__(256) k_gmm_params(ParamsArgs p) {
     {
         const int c = tid >> 1, h = tid & 1;
         const double pdc = c < d ? pd[c] : 0.0;
-        // rows r and r - 1 per round: both dots over q > r share the loads of P[q][c]; then
-        // P[r - 1][c] adds U[r - 1][r] P[r][c] (half the dependent rounds)
         int r = d - 2;
-        for (; r >= 1; r -= 2) {
-            const int r1 = r - 1;
-            double pa = 0.0, pb = 0.0;
-            if (c < d && c > r) {
-                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-                double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
-                int q = r + 1 + h;
-                for (; q + 6 < c; q += 8) {
-                    const double p0 = A[c * LD + q], p1 = A[c * LD + q + 2];
-                    const double p2 = A[c * LD + q + 4], p3 = A[c * LD + q + 6];
-                    a0 += A[r * LD + q] * p0;
-                    a1 += A[r * LD + q + 2] * p1;
-                    a2 += A[r * LD + q + 4] * p2;
-                    a3 += A[r * LD + q + 6] * p3;
-                    b0 += A[r1 * LD + q] * p0;
-                    b1 += A[r1 * LD + q + 2] * p1;
-                    b2 += A[r1 * LD + q + 4] * p2;
-                    b3 += A[r1 * LD + q + 6] * p3;
-                }
-                for (; q <= c; q += 2) {
-                    const double pq = q == c ? pdc : A[c * LD + q];
-                    a0 += A[r * LD + q] * pq;
-                    b0 += A[r1 * LD + q] * pq;
-                }
-                pa = (a0 + a1) + (a2 + a3);
-                pb = (b0 + b1) + (b2 + b3);
-            }
-            const double oa = __shfl_xor(pa, 1), ob = __shfl_xor(pb, 1);
-            if (h == 0 && c < d && c >= r) {
-                const double prc = c > r ? -(pa + oa) * pd[r] : pd[r];  // P[r][c]
-                if (c > r) A[c * LD + r] = prc;
-                A[c * LD + r1] = -(A[r1 * LD + r] * prc + (pb + ob)) * pd[r1];
-            }
+        for (; r >= kParamsInvR - 1; r -= kParamsInvR)
+            inv_rows<kParamsInvR>(A, LD, d, r, c, h, pdc, pd);
+        if (kParamsInvR > 2 && r >= 1) {
+            inv_rows<2>(A, LD, d, r, c, h, pdc, pd);
+            r -= 2;
         }
-        if (r == 0) {  // the last row of an even d, alone
-            double part = 0.0;
-            if (c < d && c > r) {
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-                int q = r + 1 + h;
-                for (; q + 6 < c; q += 8) {
-                    s0 += A[r * LD + q] * A[c * LD + q];
-                    s1 += A[r * LD + q + 2] * A[c * LD + q + 2];
-                    s2 += A[r * LD + q + 4] * A[c * LD + q + 4];
-                    s3 += A[r * LD + q + 6] * A[c * LD + q + 6];
-                }
-                for (; q <= c; q += 2) s0 += A[r * LD + q] * (q == c ? pdc : A[c * LD + q]);
-                part = (s0 + s1) + (s2 + s3);
-            }
-            const double other = __shfl_xor(part, 1);
-            if (h == 0 && c < d && c > r) A[c * LD + r] = -(part + other) * pd[r];
-        }
+        if (r == 0) inv_rows<1>(A, LD, d, r, c, h, pdc, pd);
     }
     __syncthreads();
     // prec_chol (upper): row r, column c > r at A[c][r], pd on the diagonal
