@@ -941,18 +941,27 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce(const float *part, float
     }
 }
 
-// The 32-wide-tile kernels' partials hold only the upper tiles (CovArgs::upper_only): thread q
-// sums entries 4 q .. 4 q + 3 of a row of an upper tile over the chunks (16-byte loads, in chunk
-// order) and writes them and their mirror images; lower-tile threads return.
+// The 32-wide-tile kernels' partials hold only the upper tiles (CovArgs::upper_only): the threads
+// cover the upper tiles only -- thread q of component k takes upper tile t = (q / 256) % NTU
+// (row-major order of the upper triangle), row r = (q % 256) / 8 and columns 4 g .. 4 g + 3
+// (g = q % 8) of it, eight lanes per 128-byte tile row -- sums them over the chunks (16-byte loads,
+// eight chunks in flight, in chunk order) and writes them and their mirror images.
 template <int D>
 __global__ void __launch_bounds__(256) k_gmm_cov_reduce_upper(const float *part, float *out,
-                                                              int64_t n, int chunks) {
+                                                                int64_t n, int chunks, int K) {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int NT = D / 32, NTU = NT * (NT + 1) / 2;
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (4 * q >= n) return;
-    const int e = (int)((4 * q) % (D * D)), i = e / D, j = e % D;
-    if ((j >> 5) < (i >> 5)) return;  // a lower tile: the mirror of an upper one
-    const f32x4 *p = reinterpret_cast<const f32x4 *>(part) + q;
+    if (q >= (int64_t)K * NTU * 256) return;
+    const int k = (int)(q / (NTU * 256)), w = (int)(q % 256);
+    int t = (int)((q / 256) % NTU), ti = 0;
+    while (t >= NT - ti) {  // upper tile t -> (ti, tj), tj >= ti
+        t -= NT - ti;
+        ++ti;
+    }
+    const int tj = ti + t, i = 32 * ti + w / 8, j = 32 * tj + 4 * (w % 8);
+    const int64_t e = (int64_t)k * D * D + (int64_t)i * D + j;
+    const f32x4 *p = reinterpret_cast<const f32x4 *>(part + e);
     const int64_t stride = n / 4;
     f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
     int c = 0;
@@ -964,11 +973,11 @@ __global__ void __launch_bounds__(256) k_gmm_cov_reduce_upper(const float *part,
         for (int u = 0; u < 8; ++u) s += v[u];
     }
     for (; c < chunks; ++c) s += p[(int64_t)c * stride];
-    reinterpret_cast<f32x4 *>(out)[q] = s;
-    if ((j >> 5) > (i >> 5)) {
-        float *m = out + (4 * q - e) + (int64_t)j * D + i;  // (j, i) of the same component
+    *reinterpret_cast<f32x4 *>(out + e) = s;
+    if (tj > ti) {
+        float *m = out + (int64_t)k * D * D + (int64_t)j * D + i;  // (j, i)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) m[(int64_t)t * D] = s[t];
+        for (int u = 0; u < 4; ++u) m[(int64_t)u * D] = s[u];
     }
 }
 
@@ -986,13 +995,14 @@ static int launch_cov_reduce(const float *part, float *out, int64_t n, int chunk
 
 static int launch_cov_reduce_upper(const float *part, float *out, int64_t n, int chunks, int d,
                                    hipStream_t stream) {
-    const unsigned grid = (unsigned)((n + 1023) / 1024);
+    const int K = (int)(n / ((int64_t)d * d)), ntu = (d / 32) * (d / 32 + 1) / 2;
+    const unsigned grid = (unsigned)(((int64_t)K * ntu * 256 + 255) / 256);
     if (d == 64)
         hipLaunchKernelGGL(k_gmm_cov_reduce_upper<64>, dim3(grid), dim3(256), 0, stream, part, out,
-                           n, chunks);
+                           n, chunks, K);
     else
         hipLaunchKernelGGL(k_gmm_cov_reduce_upper<128>, dim3(grid), dim3(256), 0, stream, part,
-                           out, n, chunks);
+                           out, n, chunks, K);
     return hip_error(hipGetLastError(), "k_gmm_cov_reduce_upper launch");
 }
 
